@@ -1,0 +1,268 @@
+"""GPU parity tests: the HIP kernels (librc_amd.so, through the C ABI) against the CPU oracle.
+
+Bar: bit-exact bytes, lengths and flags for every chunk (integer/byte work).  Small cases are
+compared chunk by chunk with oracle/rc_oracle.c; full-size cases use encode -> decode round
+trips plus a seeded sample of chunks checked against the oracle.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import range_coder_rust_amd as rc  # noqa: E402
+from range_coder_rust_amd import synth  # noqa: E402
+from oracle import cpu  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return rc.default_context(0)
+
+
+def dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to("cuda")
+
+
+def cum_of(c):
+    c = np.asarray(c, dtype=np.uint64)
+    return np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.uint32)
+
+
+def run_encode(model, chunks, caps, misalign=False, seed=0):
+    """Encode with chunks at contiguous ragged offsets.  If misalign, prefix the arena with a
+    random number of bytes so every chunk (and slot) starts at an arbitrary alignment."""
+    rng = np.random.default_rng(seed)
+    n = len(chunks)
+    lens = np.array([len(c) for c in chunks], np.int64)
+    base_s = int(rng.integers(0, 16)) if misalign else 0
+    sym_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64) + base_s
+    syms = np.concatenate([rng.integers(0, 256, base_s).astype(np.uint8)] +
+                          [np.asarray(c, np.uint8) for c in chunks] + [np.zeros(1, np.uint8)])
+    caps = np.asarray(caps, np.int64)
+    base_o = int(rng.integers(0, 16)) if misalign else 0
+    out_off = np.concatenate([[0], np.cumsum(caps)]).astype(np.int64) + base_o
+    out = torch.full((int(out_off[-1]) + 16,), 0xEE, dtype=torch.uint8, device="cuda")
+    out_len, flags = rc.encode_batch(model, dev(syms), dev(sym_off), out, dev(out_off))
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), out_off, out_len.cpu().numpy(), flags.cpu().numpy()
+
+
+def run_decode(model, codes, counts, misalign=False, seed=0, code_lens=None):
+    rng = np.random.default_rng(seed)
+    n = len(codes)
+    clen = np.array([len(c) for c in codes], np.int64) if code_lens is None else code_lens
+    gaps = rng.integers(0, 16, n) if misalign else np.zeros(n, np.int64)
+    coff = np.zeros(n, np.int64)
+    parts = []
+    pos = 0
+    for k, c in enumerate(codes):
+        parts.append(rng.integers(0, 256, int(gaps[k])).astype(np.uint8))
+        pos += int(gaps[k])
+        coff[k] = pos
+        parts.append(np.frombuffer(bytes(c), np.uint8))
+        pos += len(c)
+    parts.append(np.zeros(16, np.uint8))
+    blob = np.concatenate(parts)
+    counts = np.asarray(counts, np.int64)
+    base = int(rng.integers(0, 16)) if misalign else 0
+    sym_off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64) + base
+    syms = torch.full((int(sym_off[-1]) + 16,), 0xEE, dtype=torch.uint8, device="cuda")
+    flags = rc.decode_batch(model, dev(blob), dev(coff), dev(clen), syms, dev(sym_off))
+    torch.cuda.synchronize()
+    s = syms.cpu().numpy()
+    return [s[sym_off[k]:sym_off[k + 1]] for k in range(n)], flags.cpu().numpy()
+
+
+# ----------------------------------------------------------------------------- tests
+def test_known_answer_vectors_gpu(ctx):
+    kats = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kat.json")))
+    for k in kats:
+        m = rc.StaticModel(k["c"], k["cum"], k["total"])
+        code = rc.encode_chunks(m, [bytes(k["symbols"])])[0]
+        assert code.hex() == k["encoded_hex"], k["name"]
+        dec = rc.decode_chunks(m, [code], [len(k["symbols"])])[0]
+        assert list(dec) == k["symbols"], k["name"]
+
+
+def test_sample_impl_gpu(ctx):
+    """examples/sample_impl.rs:72-128 through the mirrored Encoder/Decoder/FreqTable API."""
+    test_data = [2, 1, 1, 4, 1, 4, 2, 1, 0, 1, 5, 9, 8, 7, 6, 5]
+    sd = rc.FreqTable(10)
+    for i in test_data:
+        sd.add_alphabet_freq(i)
+    sd.calc_cum()
+    encoder = rc.Encoder()
+    for i in test_data:
+        encoder.encode(sd, i)
+    code = encoder.finish()
+    assert code.hex() == "64475f8970365a2f83b20246c0"
+    decoder = rc.Decoder(code, len(test_data))
+    decodeds = [decoder.decode(sd) for _ in test_data]
+    assert decodeds == test_data
+
+
+def test_fixtures_gpu(ctx):
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "fixtures.json")))
+    for e in fx:
+        if e["config"] == "C4_adaptive":
+            continue
+        m = rc.StaticModel(e["c"], None, e["total"])
+        syms = bytes.fromhex(e["symbols_hex"])
+        code = rc.encode_chunks(m, [syms])[0]
+        assert code.hex() == e["encoded_hex"]
+        assert bytes(rc.decode_chunks(m, [code], [len(syms)])[0]) == syms
+
+
+def _random_model(rng, kind):
+    n = int(rng.choice([1, 2, 3, 7, 10, 64, 200, 255, 256]))
+    if kind == "pow2":
+        bits = int(rng.integers(max(1, int(np.ceil(np.log2(n)))), 17))
+        total = 1 << bits
+        w = rng.pareto(1.1, n) + 0.05
+        c = np.maximum(1, np.floor(w / w.sum() * total)).astype(np.int64)
+        c[int(np.argmax(c))] += total - c.sum()
+        if c.min() < 1:
+            c = np.ones(n, np.int64)
+            c[0] += total - n
+    elif kind == "big":
+        c = rng.integers(1, 1 << 23, n)
+    else:
+        c = rng.integers(1, 300, n)
+    c = c.astype(np.int64)
+    if n > 2 and kind != "pow2":
+        z = rng.random(n) < 0.15
+        z[int(np.argmax(c))] = False
+        c[z] = 0
+    return c.astype(np.uint32)
+
+
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("kind", ["pow2", "small", "big"])
+def test_random_models_vs_oracle(ctx, seed, kind):
+    rng = np.random.default_rng(1000 * seed + {"pow2": 1, "small": 2, "big": 3}[kind])
+    c = _random_model(rng, kind)
+    cum = cum_of(c)
+    total = int(c.astype(np.uint64).sum())
+    m = rc.StaticModel(c, cum, total)
+    nz = np.nonzero(c)[0]
+    p = c[nz] / c[nz].sum()
+    lens = list(rng.choice([0, 1, 2, 7, 15, 16, 17, 31, 33, 100, 257, 1000, 4099], 70))
+    chunks = [rng.choice(nz, L, p=p).astype(np.uint8) for L in lens]
+    bits = m.max_bits_per_symbol()
+    caps = [rc.slot_capacity(L, bits + 1) for L in lens]
+    out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=(seed % 2 == 1), seed=seed)
+    codes = []
+    for k, ch in enumerate(chunks):
+        f, b, L = cpu.encode(c, cum, total, ch)
+        assert (fl[k], ol[k]) == (f, L), (k, fl[k], f, ol[k], L)
+        got = bytes(out[out_off[k]: out_off[k] + ol[k]])
+        assert got == b, k
+        # bytes after the stream inside the slot are untouched
+        assert (out[out_off[k] + ol[k]: out_off[k + 1]] == 0xEE).all()
+        codes.append(b)
+    dec, fd = run_decode(m, codes, lens, misalign=(seed % 2 == 0), seed=seed + 1)
+    for k, ch in enumerate(chunks):
+        assert fd[k] == 0
+        assert (dec[k] == ch).all(), k
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_garbage_streams_decode_like_oracle(ctx, seed):
+    """find_index on arbitrary bytes (data < lower_bound wraps, rfreq >= total) must pick the
+    same index as the reference's binary search, and flag where the reference would hang."""
+    rng = np.random.default_rng(seed)
+    for kind in ["pow2", "small", "big"]:
+        c = _random_model(rng, kind)
+        cum = cum_of(c)
+        total = int(c.astype(np.uint64).sum())
+        m = rc.StaticModel(c, cum, total)
+        codes = [rng.integers(0, 256, int(rng.integers(8, 400))).astype(np.uint8).tobytes()
+                 for _ in range(64)]
+        counts = [int(rng.integers(0, 300)) for _ in codes]
+        dec, fd = run_decode(m, codes, counts, misalign=True, seed=seed)
+        for k in range(len(codes)):
+            f, d = cpu.decode(c, cum, total, codes[k], counts[k])
+            assert fd[k] == f, (kind, k, fd[k], f)
+            if f == 0:
+                assert (dec[k] == d).all(), (kind, k)
+
+
+def test_error_flags_gpu(ctx):
+    c = np.array([1, 5, 2, 0, 2, 2, 1, 1, 1, 1], np.uint32)
+    cum = cum_of(c)
+    m = rc.StaticModel(c, cum, 16)
+    chunks = [np.array([1, 3, 2], np.uint8), np.array([1, 10], np.uint8),
+              np.array([1, 2, 4, 5] * 10, np.uint8), np.array([], np.uint8),
+              np.array([3, 10], np.uint8)]
+    caps = [64, 64, 5, 64, 64]
+    out, out_off, ol, fl = run_encode(m, chunks, caps)
+    assert list(fl) == [rc.api.N.F_ZERO_FREQ, rc.api.N.F_BAD_SYMBOL, rc.api.N.F_CAPACITY, 0,
+                        rc.api.N.F_ZERO_FREQ]
+    f, full, L = cpu.encode(c, cum, 16, chunks[2])
+    assert ol[2] == L and bytes(out[out_off[2]:out_off[2] + 5]) == full[:5]
+    assert (out[out_off[2] + 5: out_off[3]] == 0xEE).all()
+    assert bytes(out[out_off[3]:out_off[3] + 8]) == bytes(8) and ol[3] == 8
+    # decoder: truncated streams and short codes
+    codes = [full[:7], full[:-1], full, full[:8]]
+    counts = [1, 40, 40, 40]
+    dec, fd = run_decode(m, codes, counts)
+    for k in range(len(codes)):
+        assert fd[k] == cpu.decode(c, cum, 16, codes[k], counts[k])[0]
+    assert fd[0] == rc.api.N.F_TRUNCATED and fd[1] == rc.api.N.F_TRUNCATED and fd[2] == 0
+    with pytest.raises(rc.ZeroFrequencyError):
+        rc.encode_chunks(m, [bytes([1, 3])])
+    with pytest.raises(rc.TruncatedStreamError):
+        rc.decode_chunks(m, [full[:-1]], [40])
+    with pytest.raises(ValueError):
+        rc.StaticModel([1, 2], [0, 2], 3)  # cum[1] != cum[0] + c[0]
+
+
+def test_synth_matches_host(ctx):
+    for (c, _, _), L in ((synth.uniform_table(), 4096), (synth.zipf_table(), 1000)):
+        inv = synth.inverse_cdf(c)
+        n = 37
+        t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+        synth.fill(ctx, 0x5EED0001, inv, t, L, n)
+        h = t.cpu().numpy()
+        for k in (0, 1, 17, 36):
+            assert (h[k * L:(k + 1) * L] == synth.host_chunk(0x5EED0001, inv, k, L)).all()
+
+
+@pytest.mark.parametrize("cfg", ["uniform", "zipf"])
+def test_full_size_round_trip(ctx, cfg):
+    """64 KiB chunks (BASELINE configs[1]/[2]) at 8192 chunks: GPU round trip over all chunks,
+    plus 24 seeded chunks bit-checked against the oracle."""
+    c, cum, total = synth.uniform_table() if cfg == "uniform" else synth.zipf_table()
+    m = rc.StaticModel(c, cum, total)
+    inv = synth.inverse_cdf(c)
+    n, L = 8192, 65536
+    syms = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    synth.fill(ctx, 0x5EED0001, inv, syms, L, n)
+    sym_off = torch.arange(n + 1, dtype=torch.int64, device="cuda") * L
+    cap = rc.slot_capacity(L, 8.0 if cfg == "uniform" else 6.0, slack=1.05)
+    out_off = torch.arange(n + 1, dtype=torch.int64, device="cuda") * cap
+    out = torch.empty(n * cap, dtype=torch.uint8, device="cuda")
+    out_len, flags = rc.encode_batch(m, syms, sym_off, out, out_off)
+    dec = torch.empty_like(syms)
+    fd = rc.decode_batch(m, out, out_off[:-1].contiguous(), out_len, dec, sym_off)
+    torch.cuda.synchronize()
+    assert int(flags.abs().sum()) == 0 and int(fd.abs().sum()) == 0
+    assert torch.equal(dec, syms)
+    ol = out_len.cpu().numpy()
+    rng = random.Random(5)
+    for k in sorted(rng.sample(range(n), 24)):
+        ch = synth.host_chunk(0x5EED0001, inv, k, L)
+        f, b, Lb = cpu.encode(c, cum, total, ch)
+        assert f == 0 and Lb == ol[k]
+        assert bytes(out[k * cap: k * cap + Lb].cpu().numpy()) == b
