@@ -1,0 +1,282 @@
+#!/usr/bin/env python3
+"""Benchmark of the batched range coder hot path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 2^20 independent 64 KiB chunks per GPU, uniform-256 static
+PModel (c[i] = 1, total 256), synthetic symbols generated in HBM.  One step = encode every chunk
+(reference: Encoder::new + 65,536 x encode + finish, encoder.rs:14-46) then decode every chunk
+(Decoder::new + 65,536 x decode, decoder.rs:14-54), all inputs resident in HBM.
+value = symbols round-tripped / second over all ranks = N_sym / (t_enc + t_dec), Gsymbols/s.
+
+N > 1 (torchrun, one process per GPU): every rank codes its own 2^20 chunks (chunks are
+independent streams — no data-path collective; weak scaling).  The torch.distributed process
+group (RCCL) is used only for the barrier and the max-over-ranks of the timed region.
+
+Also reported: the Zipf(1.2) configuration (configs[2]) on the same buffers, per-kernel times,
+the HBM roofline of the dominant kernel and a CPU baseline (the C oracle on the host cores,
+rank 0, N = 1 only, on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SEED = 0x5EED0001
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU")
+    p.add_argument("--chunk-bytes", type=int, default=65536)
+    p.add_argument("--config", choices=["uniform", "zipf"], default="uniform")
+    p.add_argument("--no-zipf", action="store_true", help="skip the secondary Zipf leg")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU sample wall time")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    return p.parse_args()
+
+
+def table(cfg):
+    from range_coder_rust_amd import synth
+    return synth.uniform_table() if cfg == "uniform" else synth.zipf_table()
+
+
+class Leg:
+    """One configuration resident in HBM: inputs, code slots, decoded output."""
+
+    def __init__(self, torch, rc, synth, ctx, cfg, n, L, rank, bufs=None):
+        c, cum, total = table(cfg)
+        self.cfg, self.n, self.L = cfg, n, L
+        self.model = rc.StaticModel(c, cum, total, ctx=ctx)
+        self.c, self.cum, self.total = c, cum, total
+        dev = torch.device("cuda", ctx.device)
+        cap = rc.slot_capacity(L, 8.0, slack=1.02)  # >= the uniform model's 8 bits/symbol
+        self.cap = cap
+        if bufs is None:
+            bufs = dict(syms=torch.empty(n * L, dtype=torch.uint8, device=dev),
+                        out=torch.empty(n * cap, dtype=torch.uint8, device=dev),
+                        dec=torch.empty(n * L, dtype=torch.uint8, device=dev))
+        self.bufs = bufs
+        self.syms, self.out, self.dec = bufs["syms"], bufs["out"], bufs["dec"]
+        self.inv = synth.inverse_cdf(c)
+        self.seed = SEED ^ (rank << 40)
+        synth.fill(ctx, self.seed, self.inv, self.syms, L, n)
+        self.sym_off = torch.arange(n + 1, dtype=torch.int64, device=dev) * L
+        self.out_off = torch.arange(n + 1, dtype=torch.int64, device=dev) * cap
+        self.code_off = self.out_off[:-1].contiguous()
+        self.out_len = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.fenc = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.fdec = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.rc = rc
+
+    def encode(self):
+        self.rc.encode_batch(self.model, self.syms, self.sym_off, self.out, self.out_off,
+                             self.out_len, self.fenc)
+
+    def decode(self):
+        self.rc.decode_batch(self.model, self.out, self.code_off, self.out_len, self.dec,
+                             self.sym_off, self.fdec)
+
+
+def equal_chunked(torch, a, b, step=1 << 30):
+    """torch.equal without a full-size temporary (the tensors are 64 GiB each)."""
+    if a.numel() != b.numel():
+        return False
+    for i in range(0, a.numel(), step):
+        if not torch.equal(a[i:i + step], b[i:i + step]):
+            return False
+    return True
+
+
+def run_leg(torch, dist, leg, steps, warmup, world):
+    """W untimed steps, then exactly K timed steps bracketed by barrier + synchronize."""
+    for _ in range(warmup):
+        leg.encode()
+        leg.decode()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1, e2 in ev:
+        e0.record()
+        leg.encode()
+        e1.record()
+        leg.decode()
+        e2.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    # correctness of the timed work: no chunk flagged, decode(encode(x)) == x
+    ok = (int(leg.fenc.abs().sum()) == 0 and int(leg.fdec.abs().sum()) == 0
+          and equal_chunked(torch, leg.dec, leg.syms))
+    code_bytes = int(leg.out_len.sum())
+    return dict(t=t, enc_ms=enc_ms, dec_ms=dec_ms, ok=ok, code_bytes=code_bytes)
+
+
+def cpu_baseline(torch, leg, seconds, threads):
+    """The C oracle (a bit-exact restatement of the Rust reference) on host cores, on a bounded
+    sample of the same chunks (copied from HBM), encode + decode, Gsymbols/s round trip."""
+    from oracle import cpu
+    L = leg.L
+
+    def run(S):
+        syms = leg.syms[: S * L].cpu().numpy()
+        so = (np.arange(S + 1) * L).astype(np.uint64)
+        oo = (np.arange(S + 1) * leg.cap).astype(np.uint64)
+        t0 = time.perf_counter()
+        out, ol, fl = cpu.encode_batch(leg.c, leg.cum, leg.total, syms, so, oo, threads)
+        t1 = time.perf_counter()
+        dec, fd = cpu.decode_batch(leg.c, leg.cum, leg.total, out, oo[:-1], ol, so, threads)
+        t2 = time.perf_counter()
+        assert (fl == 0).all() and (fd == 0).all() and (dec == syms).all()
+        # the CPU stream equals the GPU stream byte for byte on the sample's first chunks
+        g = leg.out[: leg.cap * min(S, 8)].cpu().numpy()
+        for k in range(min(S, 8)):
+            assert bytes(g[k * leg.cap: k * leg.cap + int(ol[k])]) == \
+                bytes(out[k * leg.cap: k * leg.cap + int(ol[k])])
+        return t1 - t0, t2 - t1
+
+    S0 = max(threads, 16)
+    te, td = run(S0)
+    S = int(min(leg.n, max(S0, min(32768, S0 * seconds / max(te + td, 1e-6)))))
+    S = max(threads, S // threads * threads)
+    te, td = run(S)
+    n_sym = S * L
+    return dict(value=n_sym / (te + td) / 1e9, unit="Gsymbols/s", cores=threads, kind="port",
+                sample=f"{S} of the {leg.n} 64 KiB chunks ({n_sym} symbols), encode+decode by "
+                       f"the C oracle on {threads} host threads: enc {n_sym / te / 1e9:.4f} "
+                       f"Gsym/s, dec {n_sym / td / 1e9:.4f} Gsym/s",
+                encode=n_sym / te / 1e9, decode=n_sym / td / 1e9)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import range_coder_rust_amd as rc
+    from range_coder_rust_amd import synth
+    ctx = rc.default_context(local)
+
+    n, L = args.chunks, args.chunk_bytes
+    leg = Leg(torch, rc, synth, ctx, args.config, n, L, rank)
+    res = run_leg(torch, dist, leg, args.steps, args.warmup, world)
+    n_sym_all = n * L * world
+    value = n_sym_all * args.steps / res["t"] / 1e9
+
+    # algorithmic bytes per launch: encode reads N symbols + writes the code, decode reads the
+    # code + writes N symbols; identical for both kernels
+    alg_bytes = n * L + res["code_bytes"]
+    kern = {
+        "encode": dict(ms=res["enc_ms"], gsym_s=n * L / res["enc_ms"] / 1e6,
+                       gbps=alg_bytes / res["enc_ms"] / 1e6),
+        "decode": dict(ms=res["dec_ms"], gsym_s=n * L / res["dec_ms"] / 1e6,
+                       gbps=alg_bytes / res["dec_ms"] / 1e6),
+    }
+    dom = "decode" if res["dec_ms"] >= res["enc_ms"] else "encode"
+    traffic = None
+    try:
+        with open(args.traffic) as f:
+            tr = json.load(f)
+        key = f"{args.config}:{n}:{L}:{dom}"
+        if key in tr:
+            traffic = tr[key]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        traffic = None
+    achieved = kern[dom]["gbps"]
+    roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBPS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic, kernel=dom,
+                    alg_bytes_per_launch=alg_bytes)
+
+    extras = {}
+    if not args.no_zipf and args.config == "uniform":
+        z = Leg(torch, rc, synth, ctx, "zipf", n, L, rank, bufs=leg.bufs)
+        zr = run_leg(torch, dist, z, max(2, args.steps // 2), 1, world)
+        zb = n * L + zr["code_bytes"]
+        extras["zipf1.2"] = dict(
+            value=round(n_sym_all * max(2, args.steps // 2) / zr["t"] / 1e9, 3),
+            encode_gsym_s=round(n * L / zr["enc_ms"] / 1e6, 3),
+            decode_gsym_s=round(n * L / zr["dec_ms"] / 1e6, 3),
+            encode_ms=round(zr["enc_ms"], 3), decode_ms=round(zr["dec_ms"], 3),
+            bytes_per_symbol=round(zr["code_bytes"] / (n * L), 5),
+            roofline_frac_encode=round(zb / zr["enc_ms"] / 1e6 / HBM_PEAK_GBPS, 4),
+            roofline_frac_decode=round(zb / zr["dec_ms"] / 1e6 / HBM_PEAK_GBPS, 4),
+            bit_exact_round_trip=zr["ok"])
+        # restore the headline inputs for the CPU baseline sample
+        synth.fill(ctx, leg.seed, leg.inv, leg.syms, L, n)
+        leg.encode()
+        torch.cuda.synchronize()
+
+    cpu_b = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cpu_b = cpu_baseline(torch, leg, args.cpu_seconds, threads)
+
+    if rank == 0:
+        line = {
+            "metric": "Gsymbols/s encode+decode, 256-sym static model, 64KiB chunks, 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "Gsymbols/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(res["t"] / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {"workload": f"configs[1]: {n} x {L // 1024} KiB chunks per GPU, "
+                                   f"{'uniform-256 static (c=1, total=256)' if args.config == 'uniform' else 'Zipf(1.2) static (total 2^16)'}, "
+                                   "encode then decode, inputs resident in HBM",
+                       "chunks_per_gpu": n, "chunk_symbols": L, "alphabet": 256,
+                       "total_freq": int(leg.total), "parallelism": f"chunk-shard x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu_b,
+            "encode_gsym_s": round(kern["encode"]["gsym_s"], 3),
+            "decode_gsym_s": round(kern["decode"]["gsym_s"], 3),
+            "encode_ms": round(res["enc_ms"], 3),
+            "decode_ms": round(res["dec_ms"], 3),
+            "bytes_per_symbol": round(res["code_bytes"] / (n * L), 5),
+            "bit_exact_round_trip": res["ok"],
+            "extras": extras,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not res["ok"]:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

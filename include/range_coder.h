@@ -68,6 +68,8 @@ rc_status rc_ctx_set_stream(rc_ctx* ctx, void* hip_stream);
 rc_status rc_ctx_reset_stream(rc_ctx* ctx);
 rc_status rc_ctx_synchronize(rc_ctx* ctx);
 const char* rc_status_string(rc_status s);
+/* Text of the last HIP runtime error seen by this thread ("" if none) */
+const char* rc_last_error(void);
 /* Library / device info: writes a short NUL-terminated description (arch, CUs) */
 rc_status rc_device_info(int device, char* buf, size_t buf_len);
 

@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librc_amd.so")
+LIB_PATH = os.environ.get("RC_LIB_PATH") or os.path.join(_HERE, "librc_amd.so")
 
 RC_OK = 0
 RC_E_ARG = -1
@@ -26,7 +26,7 @@ F_CORRUPT = 16
 EXPORTS = (
     "rc_ctx_create", "rc_ctx_destroy", "rc_ctx_set_stream", "rc_ctx_reset_stream",
     "rc_ctx_synchronize",
-    "rc_status_string", "rc_device_info", "rc_model_create_static", "rc_model_create_adaptive",
+    "rc_status_string", "rc_last_error", "rc_device_info", "rc_model_create_static", "rc_model_create_adaptive",
     "rc_model_destroy", "rc_encode_batch", "rc_decode_batch", "rc_encode_host",
     "rc_decode_host", "rc_synth_fill",
 )
@@ -63,6 +63,8 @@ def load():
     L.rc_ctx_synchronize.argtypes = [_P]
     L.rc_status_string.argtypes = [_I]
     L.rc_status_string.restype = ctypes.c_char_p
+    L.rc_last_error.argtypes = []
+    L.rc_last_error.restype = ctypes.c_char_p
     L.rc_device_info.argtypes = [_I, ctypes.c_char_p, ctypes.c_size_t]
     L.rc_model_create_static.argtypes = [_P, _U32, _P, _P, _U32, ctypes.POINTER(_P)]
     L.rc_model_create_adaptive.argtypes = [_P, _U32, _U32, _U32, ctypes.POINTER(_P)]
@@ -73,7 +75,7 @@ def load():
     L.rc_decode_host.argtypes = [_P, _P, _P, _P, _P, _P, _P, _U32, _P]
     L.rc_synth_fill.argtypes = [_P, _U64, _P, _P, _U64, _U32]
     for name in EXPORTS:
-        if name != "rc_status_string":
+        if name not in ("rc_status_string", "rc_last_error"):
             getattr(L, name).restype = _I
     _lib = L
     return L
@@ -85,7 +87,8 @@ def status_string(code):
 
 class RCError(RuntimeError):
     def __init__(self, code, what):
-        super().__init__(f"{what}: {status_string(code)} ({code})")
+        detail = load().rc_last_error().decode() if code == RC_E_DEVICE else ""
+        super().__init__(f"{what}: {status_string(code)} ({code}) {detail}".rstrip())
         self.code = code
 
 

@@ -37,6 +37,13 @@ typedef uint32_t u32;
 
 enum { DIV_POW2 = 0, DIV_MAGIC = 1 };
 
+// VGPR allocation floor.  On this gfx950 stack a kernel allocated 88 VGPRs (an odd number of
+// 8-register granules) corrupts co-resident waves on the same SIMD, while the identical
+// instruction stream allocated 96 VGPRs is correct.  Each kernel clobbers a
+// register so its allocation is a multiple of 16; build() rejects any other count.
+#define RC_VGPR_FLOOR_96() asm volatile("; vgpr floor 96" ::: "v95")
+#define RC_VGPR_FLOOR_64() asm volatile("; vgpr floor 64" ::: "v63")
+
 struct ModelArgs {
   const uint2* tab;  // [256] (cum, c); entries s >= n_symbols hold (0xFFFFFFFF, 0)
   const u32* lut;    // decoder buckets: s0 | s1 << 8 | split << 16
@@ -179,10 +186,12 @@ __global__ __launch_bounds__(WG) void k_encode_static(ModelArgs m, const uint8_t
   __shared__ u32 s_ring[WAVES * ENC_RING * 64];
   const u32 tid = threadIdx.x;
   s_tab[tid] = m.tab[tid];
+
   __syncthreads();
   const u32 k = blockIdx.x * WG + tid;
   if (k >= n_chunks) return;
 
+  RC_VGPR_FLOOR_96();
   const u32 lane = tid & 63, wave = tid >> 6;
   EncIO io;
   io.ring = s_ring + wave * ENC_RING * 64 + lane;
@@ -379,6 +388,7 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   const u32 k = blockIdx.x * WG + tid;
   if (k >= n_chunks) return;
 
+  RC_VGPR_FLOOR_96();
   const u32 lane = tid & 63, wave = tid >> 6;
   DecIO io;
   io.ring = s_ring + wave * DEC_RING_ALLOC * 64 + lane;
@@ -450,26 +460,28 @@ static __device__ __forceinline__ u64 mix64(u64 z) {
 __global__ __launch_bounds__(WG) void k_synth(u64 seed, const uint8_t* __restrict__ inv,
                                              uint8_t* __restrict__ dst, u64 chunk_len,
                                              u64 total_words) {
-  // one thread = 16 symbols = 4 splitmix words
-  const u64 g = (u64)blockIdx.x * WG + threadIdx.x;
+  // one item = 16 symbols = 4 splitmix words; grid-stride (a launch is capped at 2^32 items)
+  RC_VGPR_FLOOR_64();
   const u64 words_per_chunk = chunk_len >> 4;
-  if (g >= total_words) return;
-  const u64 chunk = g / words_per_chunk;
-  const u64 w16 = g - chunk * words_per_chunk;
-  u32 o[4];
+  for (u64 g = (u64)blockIdx.x * WG + threadIdx.x; g < total_words; g += (u64)gridDim.x * WG) {
+    const u64 chunk = g / words_per_chunk;
+    const u64 w16 = g - chunk * words_per_chunk;
+    u32 o[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const u64 word = mix64(seed + 0x9E3779B97F4A7C15ull * ((chunk << 32) + w16 * 4 + q + 1));
-    o[q] = (u32)inv[word & 0xFFFF] | ((u32)inv[(word >> 16) & 0xFFFF] << 8) |
-           ((u32)inv[(word >> 32) & 0xFFFF] << 16) | ((u32)inv[(word >> 48) & 0xFFFF] << 24);
+    for (int q = 0; q < 4; ++q) {
+      const u64 word = mix64(seed + 0x9E3779B97F4A7C15ull * ((chunk << 32) + w16 * 4 + q + 1));
+      o[q] = (u32)inv[word & 0xFFFF] | ((u32)inv[(word >> 16) & 0xFFFF] << 8) |
+             ((u32)inv[(word >> 32) & 0xFFFF] << 16) | ((u32)inv[(word >> 48) & 0xFFFF] << 24);
+    }
+    reinterpret_cast<uint4*>(dst + chunk * chunk_len)[w16] = make_uint4(o[0], o[1], o[2], o[3]);
   }
-  reinterpret_cast<uint4*>(dst + chunk * chunk_len)[w16] = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 __global__ __launch_bounds__(WG) void k_synth_generic(u64 seed, const uint8_t* __restrict__ inv,
                                                      uint8_t* __restrict__ dst, u64 chunk_len,
                                                      u32 n_chunks) {
   // one thread per chunk, byte stores: any chunk_len / alignment (small test inputs)
+  RC_VGPR_FLOOR_64();
   const u32 chunk = blockIdx.x * WG + threadIdx.x;
   if (chunk >= n_chunks) return;
   for (u64 i = 0; i < chunk_len; ++i) {
@@ -492,6 +504,7 @@ struct rc_ctx {
   int device;
   hipStream_t own;
   hipStream_t cur;
+  uint8_t* inv;  // 64 KiB device scratch for rc_synth_fill's inverse CDF
 };
 
 struct rc_model {
@@ -520,14 +533,23 @@ struct DeviceGuard {
 
 u32 bitlen(u32 v) { return v ? 32u - (u32)__builtin_clz(v) : 0u; }
 
+thread_local char g_last_error[256] = "";
+
+rc_status device_error(hipError_t e, const char* what) {
+  snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, hipGetErrorString(e));
+  return RC_E_DEVICE;
+}
+
 rc_status launch_status() {
   hipError_t e = hipGetLastError();
-  return e == hipSuccess ? RC_OK : RC_E_DEVICE;
+  return e == hipSuccess ? RC_OK : device_error(e, "kernel launch");
 }
 
 }  // namespace
 
 extern "C" {
+
+const char* rc_last_error(void) { return g_last_error; }
 
 const char* rc_status_string(rc_status s) {
   switch (s) {
@@ -569,6 +591,11 @@ rc_status rc_ctx_create(int device, rc_ctx** out) {
     return RC_E_DEVICE;
   }
   c->cur = c->own;
+  if (hipMalloc((void**)&c->inv, 65536) != hipSuccess) {
+    (void)hipStreamDestroy(c->own);
+    delete c;
+    return RC_E_DEVICE;
+  }
   *out = c;
   return RC_OK;
 }
@@ -577,6 +604,8 @@ rc_status rc_ctx_destroy(rc_ctx* ctx) {
   if (!ctx) return RC_E_ARG;
   DeviceGuard g(ctx->device);
   (void)hipStreamSynchronize(ctx->own);
+  (void)hipStreamSynchronize(ctx->cur);
+  (void)hipFree(ctx->inv);
   (void)hipStreamDestroy(ctx->own);
   delete ctx;
   return RC_OK;
@@ -736,9 +765,9 @@ struct DevBuf {
   void* p = nullptr;
   hipStream_t s;
   explicit DevBuf(hipStream_t st) : s(st) {}
-  bool alloc(size_t n) { return hipMallocAsync(&p, n ? n : 16, s) == hipSuccess; }
+  bool alloc(size_t n) { return hipMalloc(&p, n ? n : 16) == hipSuccess; }
   ~DevBuf() {
-    if (p) (void)hipFreeAsync(p, s);
+    if (p) (void)hipFree(p);
   }
 };
 
@@ -818,22 +847,22 @@ rc_status rc_synth_fill(rc_ctx* ctx, uint64_t seed, const uint8_t* inv_cdf_host,
   if (n_chunks == 0 || chunk_len == 0) return RC_OK;
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
-  void* dinv = nullptr;
-  if (hipMallocAsync(&dinv, 65536, ctx->cur) != hipSuccess) return RC_E_DEVICE;
-  if (hipMemcpyAsync(dinv, inv_cdf_host, 65536, hipMemcpyHostToDevice, ctx->cur) !=
-      hipSuccess)
-    return RC_E_DEVICE;
+  const uint8_t* dinv = ctx->inv;
+  hipError_t e = hipMemcpyAsync(ctx->inv, inv_cdf_host, 65536, hipMemcpyHostToDevice, ctx->cur);
+  if (e != hipSuccess) return device_error(e, "rc_synth_fill copy");
   if ((chunk_len & 15) == 0 && ((uintptr_t)syms_dev & 15) == 0) {
     const u64 words = (chunk_len >> 4) * (u64)n_chunks;
-    const u64 blocks = (words + WG - 1) / WG;
+    const u64 blocks = std::min<u64>((words + WG - 1) / WG, 1u << 16);
     hipLaunchKernelGGL(k_synth, dim3((u32)blocks), dim3(WG), 0, ctx->cur, seed,
-                       (const uint8_t*)dinv, syms_dev, chunk_len, words);
+                       dinv, syms_dev, chunk_len, words);
   } else {
     hipLaunchKernelGGL(k_synth_generic, dim3((n_chunks + WG - 1) / WG), dim3(WG), 0, ctx->cur,
-                       seed, (const uint8_t*)dinv, syms_dev, chunk_len, n_chunks);
+                       seed, dinv, syms_dev, chunk_len, n_chunks);
   }
   rc_status st = launch_status();
-  (void)hipFreeAsync(dinv, ctx->cur);
+  // the host table may be freed once the call returns: wait for the copy
+  if (st == RC_OK && (e = hipStreamSynchronize(ctx->cur)) != hipSuccess)
+    return device_error(e, "rc_synth_fill sync");
   return st;
 }
 
