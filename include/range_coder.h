@@ -96,7 +96,8 @@ rc_status rc_model_destroy(rc_model* m);
  * sym_off_dev   n_chunks+1 offsets into syms_dev
  * out_dev       output arena; chunk k's stream is written at out_off[k], capacity
  *               out_off[k+1]-out_off[k] bytes (any alignment; 16-B aligned is fastest)
- * out_len_dev   n_chunks: exact stream length (== 8 + sum of encode() return values)
+ * out_len_dev   n_chunks: exact stream length (== 8 + sum of encode() return values);
+ *               slot bytes past out_len are unspecified, nothing outside the slot is written
  * flags_dev     n_chunks: RC_F_* (0 == success)                                         */
 rc_status rc_encode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* syms_dev,
                           const uint64_t* sym_off_dev, uint32_t n_chunks, uint8_t* out_dev,

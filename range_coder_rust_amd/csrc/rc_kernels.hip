@@ -29,9 +29,9 @@ typedef uint32_t u32;
 #define TOP16 (1ull << 48)
 #define WG 256
 #define WAVES (WG / 64)
-#define ENC_RING 16          // dwords per lane in the encoder's output ring (64 B)
-#define DEC_RING 16          // dwords per lane in the decoder's input ring (64 B)
-#define DEC_RING_ALLOC 18    // + 2 mirror slots so a 12-byte window never wraps
+#define ENC_RING 32          // dwords per lane in the encoder's output ring (128 B)
+#define DEC_RING 32          // dwords per lane in the decoder's input ring (128 B)
+#define DEC_RING_ALLOC 34    // + 2 mirror slots so a 12-byte window never wraps
 #define LUT_BITS 12
 #define LUT_MAX_ENTRIES (1u << LUT_BITS)
 
@@ -43,6 +43,8 @@ enum { DIV_POW2 = 0, DIV_MAGIC = 1 };
 // register so its allocation is a multiple of 16; build() rejects any other count.
 #define RC_VGPR_FLOOR_96() asm volatile("; vgpr floor 96" ::: "v95")
 #define RC_VGPR_FLOOR_64() asm volatile("; vgpr floor 64" ::: "v63")
+#define RC_VGPR_FLOOR_128() asm volatile("; vgpr floor 128" ::: "v127")
+#define RC_VGPR_FLOOR_144() asm volatile("; vgpr floor 144" ::: "v143")
 
 struct ModelArgs {
   const uint2* tab;  // [256] (cum, c); entries s >= n_symbols hold (0xFFFFFFFF, 0)
@@ -55,6 +57,8 @@ struct ModelArgs {
   u32 lut_max;       // number of buckets - 1
   float ftotal;      // (float)total
 };
+
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
 static __device__ __forceinline__ u32 hi32(u64 v) { return (u32)(v >> 32); }
 
@@ -69,278 +73,378 @@ static __device__ __forceinline__ u64 range_par_total(u64 range, const ModelArgs
 
 // ------------------------------------------------------------------------------------------
 // Encoder
+//
+// Per lane: one chunk.  Input: 64-symbol tiles (4 x 16 B per lane, issued one tile ahead).
+// Output: settled bytes are packed into dwords and pushed into a per-lane 128-B LDS ring every
+// symbol (unconditionally: when fewer than 4 bytes are ready the push writes the next, still
+// free, slot and does not advance).  HBM writes are cooperative: when any lane's ring holds
+// FLUSH_AT bytes, the wave runs a flush round in which every lane holding a complete 64-B unit
+// hands it over; each store instruction then writes 16 chunks x 64 B (whole 64-B units), which
+// the per-lane pattern (one 16-B granule of 64 different lines per instruction) cannot.
 // ------------------------------------------------------------------------------------------
-struct EncState {
-  u64 low, range;  // RangeCoder state (range_coder.rs:7-12)
-  u64 acc;         // settled bytes not yet in the ring (newest byte in the low bits)
-  u32 nbits;       // 8 * bytes held in acc (< 32 between symbols)
-  u32 wpos;        // byte position (from the 16-B aligned slot base) of the next ring dword
-  u32 fpos;        // byte position of the next 16-B granule to store to HBM
-  u32 lo_ok, hi_ok;  // writable byte window [lo_ok, hi_ok) relative to the aligned base
-  u32 flag;
-};
+#define ENC_UNIT 64    // bytes per flush unit
+#define FLUSH_AT 88    // ring fill forcing a flush round: 88 + 7*3 + 3 + 11 (rare tail) < 124
+#define SINK_SLOTS 65536
+__device__ uint4 g_sink[SINK_SLOTS];  // target of masked-out bytes (never read)
 
-struct EncIO {
-  uint8_t* gbase;  // 16-B aligned base of the output slot
+struct Enc {
+  u64 low, range;  // RangeCoder state (range_coder.rs:7-12)
+  u64 acc;         // settled bytes not yet pushed (newest in the low bits)
+  u32 nbits;       // 8 * bytes held in acc, < 32 between symbols
+  u32 wpos;        // ring byte position of the next push (from the 64-B aligned slot base)
+  u32 fpos;        // byte position of the next unit to store
+  u32 err;         // first RC_F_* error of this chunk
   u32* ring;       // this lane's ring column: dword j at ring[j * 64]
 };
 
-static __device__ __forceinline__ void enc_push_dword(EncState& st, const EncIO& io, u32 be) {
-  io.ring[((st.wpos >> 2) & (ENC_RING - 1)) * 64] = __builtin_bswap32(be);
-  st.wpos += 4;
-}
+// Per-chunk output geometry shared with the other lanes of the wave (flush rounds)
+struct EncOut {
+  uint8_t* gbase;  // 64-B aligned base of the slot
+  u32 lo_ok, hi_ok;  // writable byte window [lo_ok, hi_ok) relative to gbase
+};
 
-// Store granule [fpos, fpos + 16) from the ring; bytes outside [lo_ok, hi_ok) are skipped.
-static __device__ __forceinline__ void enc_flush_one(EncState& st, const EncIO& io) {
-  const u32* rp = io.ring + ((st.fpos >> 2) & (ENC_RING - 1)) * 64;
-  uint4 v = make_uint4(rp[0], rp[64], rp[128], rp[192]);
-  if (st.fpos >= st.lo_ok && st.fpos + 16 <= st.hi_ok) {
-    *reinterpret_cast<uint4*>(io.gbase + st.fpos) = v;
-  } else {
-    u32 w[4] = {v.x, v.y, v.z, v.w};
+// One flush round.  Lane L of the wave moves granule (L & 3) of the unit of chunk 16*i + L/4
+// for i = 0..3; chunks with has == false are masked.  Granules touching the slot edges are
+// written byte by byte (first unit of a misaligned slot, capacity end).
+static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, const u32* wring,
+                                                 const EncOut* wout) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      u32 p = st.fpos + j;
-      if (p >= st.lo_ok && p < st.hi_ok) io.gbase[p] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+  for (int i = 0; i < 4; ++i) {
+    const u32 c = 16 * i + (lane >> 2), g = lane & 3;
+    const bool hc = __shfl((int)has, c) != 0;
+    const u32 fp = (u32)__shfl((int)e.fpos, c);
+    if (hc) {
+      const u32 slot = (fp >> 2) + 4 * g;
+      const u32* rp = wring + c;
+      const uint4 v = make_uint4(rp[((slot + 0) & (ENC_RING - 1)) * 64],
+                                 rp[((slot + 1) & (ENC_RING - 1)) * 64],
+                                 rp[((slot + 2) & (ENC_RING - 1)) * 64],
+                                 rp[((slot + 3) & (ENC_RING - 1)) * 64]);
+      const EncOut o = wout[c];
+      const u32 p0 = fp + 16 * g;
+      if (p0 >= o.lo_ok && p0 + 16 <= o.hi_ok) {
+        *reinterpret_cast<uint4*>(o.gbase + p0) = v;
+      } else {
+        const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const u32 p = p0 + j;
+          if (p >= o.lo_ok && p < o.hi_ok) o.gbase[p] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+        }
+      }
     }
   }
-  st.fpos += 16;
+  e.fpos += has ? (u32)ENC_UNIT : 0u;
 }
 
-static __device__ __forceinline__ void enc_flush_ready(EncState& st, const EncIO& io) {
-  while (st.wpos - st.fpos >= 16) enc_flush_one(st, io);
+// flush rounds until no lane's ring is above the threshold (wave-uniform call sites only)
+static __device__ __forceinline__ void enc_flush(Enc& e, u32 lane, const u32* wring,
+                                                 const EncOut* wout) {
+  while (__any((int)(e.wpos - e.fpos >= FLUSH_AT)))
+    enc_round(e, e.wpos - e.fpos >= ENC_UNIT, lane, wring, wout);
 }
 
-// One settled byte (left_shift, range_coder.rs:95-100, done by the caller).
-static __device__ __forceinline__ void enc_emit_byte(EncState& st, const EncIO& io, u32 b) {
-  st.acc = (st.acc << 8) | b;
-  st.nbits += 8;
-  if (st.nbits >= 32) {
-    st.nbits -= 32;
-    enc_push_dword(st, io, (u32)(st.acc >> st.nbits));
+// One settled byte, with a conditional push (rare paths only).
+static __device__ __forceinline__ void enc_emit_byte(Enc& e, u32 b) {
+  e.acc = (e.acc << 8) | b;
+  e.nbits += 8;
+  if (e.nbits >= 32) {
+    e.nbits -= 32;
+    e.ring[((e.wpos >> 2) & (ENC_RING - 1)) * 64] = __builtin_bswap32((u32)(e.acc >> e.nbits));
+    e.wpos += 4;
   }
 }
 
-// Rare paths: the no-carry loop settling >= 4 bytes, and range_reduction_expansion.
-static __device__ __forceinline__ void enc_rare(EncState& st, const EncIO& io,
-                                                          bool loop1) {
-  if (loop1) {
-    // no_carry_expansion (range_coder.rs:110-116), byte by byte
-    while (((st.low ^ (st.low + st.range)) >> 56) == 0) {
-      enc_emit_byte(st, io, (u32)(st.low >> 56));
-      st.low <<= 8;
-      st.range <<= 8;
-    }
+// Rare tail of param_update for one lane: the no-carry loop when >= 4 bytes settle
+// (range_coder.rs:110-116, continued byte by byte) and range_reduction_expansion (:126-135).
+static __device__ __forceinline__ void enc_rare(Enc& e) {
+  while (((e.low ^ (e.low + e.range)) >> 56) == 0) {
+    enc_emit_byte(e, (u32)(e.low >> 56));
+    e.low <<= 8;
+    e.range <<= 8;
   }
-  // range_reduction_expansion (range_coder.rs:126-135)
-  while (st.range < TOP16) {
-    st.range = ~st.low & (TOP16 - 1);
-    enc_emit_byte(st, io, (u32)(st.low >> 56));
-    st.low <<= 8;
-    st.range <<= 8;
+  while (e.range < TOP16) {
+    e.range = ~e.low & (TOP16 - 1);
+    enc_emit_byte(e, (u32)(e.low >> 56));
+    e.low <<= 8;
+    e.range <<= 8;
   }
-  enc_flush_ready(st, io);
 }
 
-// Encoder::encode (encoder.rs:24-37) -> RangeCoder::param_update (range_coder.rs:53-92)
+// Encoder::encode (encoder.rs:24-37) -> RangeCoder::param_update (range_coder.rs:53-92),
+// common path without branches.  Returns true when the lane needs enc_rare().
 template <int DIV>
-static __device__ __forceinline__ void enc_symbol(EncState& st, const EncIO& io,
-                                                  const ModelArgs& m, const uint2* s_tab,
-                                                  u32 sym) {
-  uint2 e = s_tab[sym];
-  u32 cum = e.x, c = e.y;
-  if (c == 0) {  // zero-frequency or out-of-alphabet symbol: flag, keep the lane finite
-    if (!st.flag) st.flag = (cum == 0xFFFFFFFFu) ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ;
-    c = 1;
-    cum = 0;
+static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, const uint2* s_tab,
+                                                u32 sym) {
+  const uint2 t = s_tab[sym];
+  const bool bad = t.y == 0;  // zero frequency (reference: endless loop) or outside alphabet
+  const u32 code = t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ;
+  e.err = (bad && e.err == 0) ? code : e.err;
+  const u32 c = bad ? 1u : t.y, cum = bad ? 0u : t.x;
+  const u64 r = range_par_total<DIV>(e.range, m);
+  e.range = r * (u64)c;   // range_coder.rs:65
+  e.low += r * (u64)cum;  // range_coder.rs:68-81 (overflow unreachable)
+  // no_carry_expansion in closed form: k = clz(low ^ upper) / 8 bytes settle (<= 3 here;
+  // x == 0 means >= 4 and the rare path continues after these 3)
+  const u32 x = hi32(e.low) ^ hi32(e.low + e.range);
+  const u32 nb = (u32)__builtin_clz(x | 1u) & 24u;
+  const u32 bytes = (u32)(((u64)hi32(e.low) << nb) >> 32);
+  e.acc = (e.acc << nb) | bytes;
+  e.low <<= nb;
+  e.range <<= nb;
+  const u32 nbits = e.nbits + nb;
+  const bool push = nbits >= 32;
+  e.nbits = push ? nbits - 32 : nbits;
+  e.ring[((e.wpos >> 2) & (ENC_RING - 1)) * 64] = __builtin_bswap32((u32)(e.acc >> e.nbits));
+  e.wpos += push ? 4u : 0u;
+  return (x == 0) | (hi32(e.range) < 0x10000u);
+}
+
+// one symbol for the lanes with `act`; the rare path (wave-uniform branch) may flush
+template <int DIV>
+static __device__ __forceinline__ void enc_sym(Enc& e, const ModelArgs& m, const uint2* s_tab,
+                                               u32 sym, bool act, u32 lane, const u32* wring,
+                                               const EncOut* wout) {
+  bool rare = false;
+  if (act) rare = enc_step<DIV>(e, m, s_tab, sym);
+  if (__builtin_expect(__any((int)rare), 0)) {
+    if (rare) enc_rare(e);
+    enc_flush(e, lane, wring, wout);
   }
-  u64 r = range_par_total<DIV>(st.range, m);
-  st.range = r * (u64)c;   // range_coder.rs:65
-  st.low += r * (u64)cum;  // range_coder.rs:68-81 (overflow unreachable)
-  u32 x = hi32(st.low) ^ hi32(st.low + st.range);
-  bool rare = (x == 0);
-  if (!rare) {
-    // no-carry loop in closed form: k = clz(x) / 8 <= 3 bytes settle
-    u32 nb = __clz(x) & 24u;
-    u32 lh = hi32(st.low);
-    st.acc = (st.acc << nb) | (u64)(u32)(((u64)lh << nb) >> 32);
-    st.nbits += nb;
-    st.low <<= nb;
-    st.range <<= nb;
-    if (st.nbits >= 32) {
-      st.nbits -= 32;
-      enc_push_dword(st, io, (u32)(st.acc >> st.nbits));
-    }
-  }
-  if (rare || st.range < TOP16) enc_rare(st, io, rare);
+}
+
+// 8 symbols from two dwords, then a flush check (wave-uniform)
+template <int DIV>
+static __device__ __forceinline__ void enc8(Enc& e, const ModelArgs& m, const uint2* s_tab,
+                                            u32 w0, u32 w1, bool act, u32 lane,
+                                            const u32* wring, const EncOut* wout) {
+  enc_sym<DIV>(e, m, s_tab, w0 & 255u, act, lane, wring, wout);
+  enc_sym<DIV>(e, m, s_tab, (w0 >> 8) & 255u, act, lane, wring, wout);
+  enc_sym<DIV>(e, m, s_tab, (w0 >> 16) & 255u, act, lane, wring, wout);
+  enc_sym<DIV>(e, m, s_tab, w0 >> 24, act, lane, wring, wout);
+  enc_sym<DIV>(e, m, s_tab, w1 & 255u, act, lane, wring, wout);
+  enc_sym<DIV>(e, m, s_tab, (w1 >> 8) & 255u, act, lane, wring, wout);
+  enc_sym<DIV>(e, m, s_tab, (w1 >> 16) & 255u, act, lane, wring, wout);
+  enc_sym<DIV>(e, m, s_tab, w1 >> 24, act, lane, wring, wout);
+  enc_flush(e, lane, wring, wout);
 }
 
 template <int DIV>
-__global__ __launch_bounds__(WG) void k_encode_static(ModelArgs m, const uint8_t* __restrict__ syms,
-                                                     const u64* __restrict__ sym_off,
-                                                     u32 n_chunks, uint8_t* __restrict__ out,
-                                                     const u64* __restrict__ out_off,
-                                                     u64* __restrict__ out_len,
-                                                     u32* __restrict__ flags) {
+static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const uint2* s_tab,
+                                             uint4 v, bool act, u32 lane, const u32* wring,
+                                             const EncOut* wout) {
+  enc8<DIV>(e, m, s_tab, v.x, v.y, act, lane, wring, wout);
+  enc8<DIV>(e, m, s_tab, v.z, v.w, act, lane, wring, wout);
+}
+
+// one symbol fetched byte-wise (unaligned head / tail of a chunk)
+template <int DIV>
+static __device__ __forceinline__ void enc_byte_sym(Enc& e, const ModelArgs& m,
+                                                    const uint2* s_tab, const uint8_t* sp, u64 i,
+                                                    bool act, u32 lane, const u32* wring,
+                                                    const EncOut* wout) {
+  const u32 sym = act ? (u32)sp[i] : 0u;
+  enc_sym<DIV>(e, m, s_tab, sym, act, lane, wring, wout);
+}
+
+template <int DIV>
+__global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint8_t* __restrict__ syms,
+                                                        const u64* __restrict__ sym_off,
+                                                        u32 n_chunks, uint8_t* __restrict__ out,
+                                                        const u64* __restrict__ out_off,
+                                                        u64* __restrict__ out_len,
+                                                        u32* __restrict__ flags) {
   __shared__ uint2 s_tab[256];
   __shared__ u32 s_ring[WAVES * ENC_RING * 64];
+  __shared__ EncOut s_out[WG];
   const u32 tid = threadIdx.x;
   s_tab[tid] = m.tab[tid];
-
-  __syncthreads();
-  const u32 k = blockIdx.x * WG + tid;
-  if (k >= n_chunks) return;
-
-  RC_VGPR_FLOOR_96();
   const u32 lane = tid & 63, wave = tid >> 6;
-  EncIO io;
-  io.ring = s_ring + wave * ENC_RING * 64 + lane;
+  const u32 k = blockIdx.x * WG + tid;
+  const bool live = k < n_chunks;  // dead lanes still take part in the wave's flush rounds
+  RC_VGPR_FLOOR_128();
 
-  const u64 s0 = sym_off[k], s1 = sym_off[k + 1];
-  const u64 o0 = out_off[k], o1 = out_off[k + 1];
-  const u32 a = (u32)(((uintptr_t)out + o0) & 15);
-  io.gbase = out + o0 - a;
+  u64 s0 = 0, n = 0, o0 = 0, o1 = 0;
+  if (live) {
+    s0 = sym_off[k];
+    n = sym_off[k + 1] - s0;
+    o0 = out_off[k];
+    o1 = out_off[k + 1];
+  }
+  const u32 a = (u32)(((uintptr_t)out + o0) & (ENC_UNIT - 1));
   u64 cap = o1 - o0;
   if (cap > 0xFFFFFF00ull - a) cap = 0xFFFFFF00ull - a;
+  s_out[tid].gbase = out + o0 - a;
+  s_out[tid].lo_ok = a;
+  s_out[tid].hi_ok = a + (u32)cap;
+  __syncthreads();
+  const u32* wring = s_ring + wave * ENC_RING * 64;
+  const EncOut* wout = s_out + wave * 64;
 
-  EncState st;
-  st.low = 0;           // RangeCoder::default (range_coder.rs:13-20)
-  st.range = ~0ull;
-  st.acc = 0;
-  st.nbits = 8 * (a & 3);  // pad bytes ahead of the slot (never stored)
-  st.wpos = a & ~3u;
-  st.fpos = 0;
-  st.lo_ok = a;
-  st.hi_ok = a + (u32)cap;
-  st.flag = 0;
+  Enc e;
+  e.low = 0;  // RangeCoder::default (range_coder.rs:13-20)
+  e.range = ~0ull;
+  e.acc = 0;
+  e.nbits = 8 * (a & 3);  // pad bytes in front of the slot (never stored)
+  e.wpos = a & ~3u;
+  e.fpos = 0;
+  e.err = 0;
+  e.ring = s_ring + wave * ENC_RING * 64 + lane;
 
   const uint8_t* sp = syms + s0;
-  const u64 n = s1 - s0;
-  u64 i = 0;
-  // head: symbols until the input pointer is 16-B aligned
-  u64 head = (16 - ((uintptr_t)sp & 15)) & 15;
+  u64 head = (64 - ((uintptr_t)sp & 63)) & 63;  // symbols before the first 64-B aligned tile
   if (head > n) head = n;
-  for (; i < head; ++i) {
-    enc_symbol<DIV>(st, io, m, s_tab, sp[i]);
-    enc_flush_ready(st, io);
+  const u64 ntile = (n - head) >> 6;
+  const u64 tail0 = head + (ntile << 6);
+  // head: byte-wise, all lanes in step (flush rounds are wave-wide)
+  for (u64 i = 0; __any((int)(i < head)); ++i) {
+    enc_byte_sym<DIV>(e, m, s_tab, sp, i, i < head, lane, wring, wout);
+    if ((i & 7) == 7) enc_flush(e, lane, wring, wout);
   }
-  // body: 16 symbols per 16-B load, next block prefetched
-  const u64 nblk = (n - i) >> 4;
-  const uint4* bp = reinterpret_cast<const uint4*>(sp + i);
-  uint4 cur = nblk ? bp[0] : make_uint4(0, 0, 0, 0);
-  for (u64 b = 0; b < nblk; ++b) {
-    uint4 nxt = bp[b + 1 < nblk ? b + 1 : b];
-    u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) enc_symbol<DIV>(st, io, m, s_tab, (w[q] >> (8 * j)) & 255u);
-      enc_flush_ready(st, io);
+  // body: 64-symbol tiles, the next one prefetched
+  const uint4* tp = reinterpret_cast<const uint4*>(sp + head);
+  uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0;
+  if (ntile) {
+    c0 = tp[0];
+    c1 = tp[1];
+    c2 = tp[2];
+    c3 = tp[3];
+  }
+  for (u64 t = 0; __any((int)(t < ntile)); ++t) {
+    const bool act = t < ntile;
+    uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
+    if (t + 1 < ntile) {
+      n0 = tp[(t + 1) * 4 + 0];
+      n1 = tp[(t + 1) * 4 + 1];
+      n2 = tp[(t + 1) * 4 + 2];
+      n3 = tp[(t + 1) * 4 + 3];
     }
-    cur = nxt;
+    enc16<DIV>(e, m, s_tab, c0, act, lane, wring, wout);
+    enc16<DIV>(e, m, s_tab, c1, act, lane, wring, wout);
+    enc16<DIV>(e, m, s_tab, c2, act, lane, wring, wout);
+    enc16<DIV>(e, m, s_tab, c3, act, lane, wring, wout);
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
   }
-  i += nblk << 4;
-  for (; i < n; ++i) {
-    enc_symbol<DIV>(st, io, m, s_tab, sp[i]);
-    enc_flush_ready(st, io);
+  for (u64 j = 0; __any((int)(tail0 + j < n)); ++j) {  // j is wave-uniform
+    enc_byte_sym<DIV>(e, m, s_tab, sp, tail0 + j, tail0 + j < n, lane, wring, wout);
+    if ((j & 7) == 7) enc_flush(e, lane, wring, wout);
   }
 
   // Encoder::finish (encoder.rs:40-46): 8 x left_shift
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    enc_emit_byte(st, io, (u32)(st.low >> 56));
-    st.low <<= 8;
+    enc_emit_byte(e, (u32)(e.low >> 56));
+    e.low <<= 8;
   }
-  const u32 len = st.wpos + (st.nbits >> 3) - a;
-  if (st.nbits) enc_push_dword(st, io, (u32)(st.acc << (32 - st.nbits)));
+  const u32 len = e.wpos + (e.nbits >> 3) - a;
+  if (e.nbits) {
+    e.ring[((e.wpos >> 2) & (ENC_RING - 1)) * 64] = __builtin_bswap32((u32)(e.acc << (32 - e.nbits)));
+    e.wpos += 4;
+  }
+  // final rounds: the last (partial) units, clipped to the stream end
   const u32 end = a + len;
-  if (end < st.hi_ok) st.hi_ok = end;
-  while (st.fpos < st.wpos) enc_flush_one(st, io);
-  if (!st.flag && (u64)len > cap) st.flag = RC_F_CAPACITY;
-  out_len[k] = len;
-  flags[k] = st.flag;
+  if (end < s_out[tid].hi_ok) s_out[tid].hi_ok = end;
+  while (__any((int)(e.fpos < e.wpos))) enc_round(e, e.fpos < e.wpos, lane, wring, wout);
+  if (live) {
+    if (!e.err && (u64)len > cap) e.err = RC_F_CAPACITY;
+    out_len[k] = len;
+    flags[k] = e.err;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
 // Decoder
+//
+// Per lane: one chunk.  The code stream is staged through a per-lane 128-B LDS ring (+2
+// mirror dwords so a 12-byte window never wraps), refilled 64 B at a time: at each 16-symbol
+// phase boundary a lane stores its 16 decoded symbols, moves its pending 64-B load into the
+// ring and, if the ring has room, issues the next 64-B load.  The pending load is therefore
+// waited for with vmcnt(1) one phase after it was issued.  Lanes that consume faster than the
+// ring covers (rare renormalisation bursts) are refilled synchronously.
 // ------------------------------------------------------------------------------------------
-struct DecState {
+struct Dec {
   u64 low, range, data;  // RangeCoder + Decoder::data (decoder.rs:6-12)
-  u32 cpos;  // bytes consumed, relative to the 16-B aligned base of the code stream
-  u32 fill;  // bytes staged into the ring, same origin
-  u32 lim;   // cpos beyond lim == more bytes consumed than the stream holds
-  u32 flag;
-};
-
-struct DecIO {
-  const uint8_t* gnext;  // next 16-B block to fetch
-  const uint8_t* glast;  // last block holding a byte of this chunk (fetch clamp)
-  uint4 pend;            // in-flight block
+  u32 cpos;   // bytes consumed, relative to the 16-B aligned base of the code stream
+  u32 fill;   // bytes staged into the ring, same origin
+  u32 lim;    // cpos > lim: more bytes consumed than the stream holds
+  u32 err;
+  u32 pend_ok;           // a 64-B load is in flight in pend[]
   u32* ring;             // this lane's ring column: dword j at ring[j * 64]
+  const uint4* gnext;    // next 16-B block of the stream
+  const uint4* glast;    // last block holding a byte of this chunk (fetch clamp)
+  uint4 pend[4];
 };
 
-static __device__ __forceinline__ void dec_refill_one(DecState& st, DecIO& io) {
-  const u32 j = (st.fill >> 2) & (DEC_RING - 1);
-  u32* rp = io.ring + j * 64;
-  rp[0] = io.pend.x;
-  rp[64] = io.pend.y;
-  rp[128] = io.pend.z;
-  rp[192] = io.pend.w;
-  if (j == 0) {  // mirror slots 16, 17
-    rp[DEC_RING * 64] = io.pend.x;
-    rp[(DEC_RING + 1) * 64] = io.pend.y;
+static __device__ __forceinline__ void dec_issue(Dec& d) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint4* p = d.gnext + q < d.glast ? d.gnext + q : d.glast;
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;  // global, not flat
+    d.pend[q] = make_uint4(v.x, v.y, v.z, v.w);
   }
-  st.fill += 16;
-  io.pend = *reinterpret_cast<const uint4*>(io.gnext);
-  io.gnext = io.gnext < io.glast ? io.gnext + 16 : io.glast;
+  d.gnext += 4;
+  d.pend_ok = 1;
 }
 
-static __device__ __forceinline__ void dec_refill_ready(DecState& st, DecIO& io) {
-  while ((int)(st.fill - st.cpos) < 24) dec_refill_one(st, io);
+static __device__ __forceinline__ void dec_commit(Dec& d) {
+  const u32 j = (d.fill >> 2) & (DEC_RING - 1);
+  u32* rp = d.ring + j * 64;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    rp[(4 * q + 0) * 64] = d.pend[q].x;
+    rp[(4 * q + 1) * 64] = d.pend[q].y;
+    rp[(4 * q + 2) * 64] = d.pend[q].z;
+    rp[(4 * q + 3) * 64] = d.pend[q].w;
+  }
+  if (j == 0) {  // mirror slots
+    rp[DEC_RING * 64] = d.pend[0].x;
+    rp[(DEC_RING + 1) * 64] = d.pend[0].y;
+  }
+  d.fill += 64;
+  d.pend_ok = 0;
+}
+
+// phase boundary: commit the pending load, issue the next one if the ring has room
+static __device__ __forceinline__ void dec_phase(Dec& d) {
+  if (d.pend_ok) dec_commit(d);
+  if ((int)(d.fill - d.cpos) <= 56) dec_issue(d);
+}
+
+// a lane about to read past the staged bytes: commit / load synchronously (rare)
+static __device__ __forceinline__ void dec_sync(Dec& d) {
+  while ((int)(d.fill - d.cpos) < 4) {
+    if (!d.pend_ok) dec_issue(d);
+    dec_commit(d);
+  }
 }
 
 // data = the 8 code bytes ending at cpos, big-endian (Decoder::shift_left_buffer, :31-35)
-static __device__ __forceinline__ void dec_window(DecState& st, const DecIO& io) {
-  const u32 p = st.cpos - 8;
-  const u32* rp = io.ring + ((p >> 2) & (DEC_RING - 1)) * 64;
+static __device__ __forceinline__ void dec_window(Dec& d) {
+  const u32 p = d.cpos - 8;
+  const u32* rp = d.ring + ((p >> 2) & (DEC_RING - 1)) * 64;
   const u32 d0 = rp[0], d1 = rp[64], d2 = rp[128];
   const u32 sh = p & 3;
   const u32 w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
   const u32 w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-  st.data = ((u64)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
+  d.data = ((u64)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
 }
 
-static __device__ __forceinline__ void dec_rare(DecState& st, DecIO& io) {
+static __device__ __forceinline__ void dec_rare(Dec& d) {
   // range_reduction_expansion (range_coder.rs:126-135); the decoder only counts the bytes
-  while (st.range < TOP16) {
-    st.range = ~st.low & (TOP16 - 1);
-    st.low <<= 8;
-    st.range <<= 8;
-    st.cpos += 1;
+  while (d.range < TOP16) {
+    d.range = ~d.low & (TOP16 - 1);
+    d.low <<= 8;
+    d.range <<= 8;
+    d.cpos += 1;
   }
-  dec_refill_ready(st, io);
 }
 
-// Decoder::decode (decoder.rs:38-54) with FreqTable::find_index (sample_impl.rs:27-45)
-template <int DIV>
-static __device__ __forceinline__ u32 dec_symbol(DecState& st, DecIO& io, const ModelArgs& m,
-                                                 const uint2* s_tab, const u32* s_lut) {
-  const u64 x = st.data - st.low;
-  const u64 r = range_par_total<DIV>(st.range, m);
-  // hint: q ~ x / r = x * total / range, from the top 32 bits of both (range >= 2^48)
-  const u32 e = __clz(hi32(st.range));
-  const u32 X = hi32(x << e), R = hi32(st.range << e);
-  float qf = (float)X * (m.ftotal * __builtin_amdgcn_rcpf((float)R));
-  qf = fminf(qf, 4.0e9f);
-  const u32 qh = (u32)qf;
-  u32 b = qh >> m.lut_shift;
-  b = b < m.lut_max ? b : m.lut_max;
-  const u32 ent = s_lut[b];
-  u32 s = ((qh - (b << m.lut_shift)) >= (ent >> 16)) ? ((ent >> 8) & 255u) : (ent & 255u);
-  uint2 t = s_tab[s];
-  u64 A = r * (u64)t.x;
-  u64 B = r * (u64)t.y;
-  // exact verification: s = #{ j in [1, n-1] : r * cum[j] <= x }  (== the reference's index)
+// the exact index: s = #{ j in [1, n-1] : r * cum[j] <= x }  (FreqTable::find_index)
+static __device__ __forceinline__ void dec_fix(u32& s, uint2& t, u64& A, u64& B, u64 x,
+                                                        u64 r, const uint2* s_tab, u32 n) {
   if (A > x) {
     do {
       --s;
@@ -348,28 +452,61 @@ static __device__ __forceinline__ u32 dec_symbol(DecState& st, DecIO& io, const 
       A = r * (u64)t.x;
     } while (A > x);
     B = r * (u64)t.y;
+  } else {
+    while (s + 1 < n && x - A >= B) {
+      ++s;
+      t = s_tab[s];
+      A = r * (u64)t.x;
+      B = r * (u64)t.y;
+    }
   }
-  while (s + 1 < m.n && x - A >= B) {
-    ++s;
-    t = s_tab[s];
-    A = r * (u64)t.x;
-    B = r * (u64)t.y;
+}
+
+// Decoder::decode (decoder.rs:38-54) with FreqTable::find_index (sample_impl.rs:27-45)
+template <int DIV>
+static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const uint2* s_tab,
+                                              const u32* s_lut) {
+  const u64 x = d.data - d.low;
+  const u64 r = range_par_total<DIV>(d.range, m);
+  // hint q ~ x / r (relative error ~2^-22): bucket table -> candidate symbol
+  // (opaque halves: keeps hipcc from re-fusing this into an exact u64->f32 conversion)
+  u32 xh = hi32(x), xl = (u32)x, rh = hi32(r), rl = (u32)r;
+  asm volatile("" : "+v"(xh), "+v"(xl), "+v"(rh), "+v"(rl));
+  const float fx = fmaf((float)xh, 4294967296.0f, (float)xl);
+  const float fr = fmaf((float)rh, 4294967296.0f, (float)rl);
+  const float qf = fminf(fx * __builtin_amdgcn_rcpf(fr), 4.0e9f);
+  const u32 qh = (u32)qf;
+  const u32 b = min(qh >> m.lut_shift, m.lut_max);
+  const u32 ent = s_lut[b];
+  u32 s = ((qh - (b << m.lut_shift)) >= (ent >> 16)) ? ((ent >> 8) & 255u) : (ent & 255u);
+  uint2 t = s_tab[s];
+  u64 A = r * (u64)t.x;
+  u64 B = r * (u64)t.y;
+  // exact verification r*cum[s] <= x < r*cum[s+1]; the hint is rarely off
+  const bool off = (A > x) | ((s + 1 < m.n) & (x - A >= B));
+  if (__builtin_expect(__any(off), 0)) {
+    if (off) dec_fix(s, t, A, B, x, r, s_tab, m.n);
   }
-  if (t.y == 0) {  // only reachable on corrupt input (reference: infinite loop)
-    // a stream already over-read would have panicked first (decoder.rs:33)
-    if (!st.flag) st.flag = st.cpos > st.lim ? RC_F_TRUNCATED : RC_F_CORRUPT;
+  if (t.y == 0) {  // only on corrupt input (reference: endless loop); an over-read came first
+    d.err = d.err ? d.err : (d.cpos > d.lim ? RC_F_TRUNCATED : RC_F_CORRUPT);
     B = r;
   }
   // param_update (range_coder.rs:53-92)
-  st.low += A;
-  st.range = B;
-  const u64 xx = st.low ^ (st.low + st.range);
-  const u32 k8 = __clzll(xx) & 56u;  // bytes settled by no_carry_expansion, x 8
-  st.low <<= k8;
-  st.range <<= k8;
-  st.cpos += k8 >> 3;
-  if (st.range < TOP16) dec_rare(st, io);
-  dec_window(st, io);
+  d.low += A;
+  d.range = B;
+  const u32 k8 = (u32)__clzll(d.low ^ (d.low + d.range)) & 56u;  // no-carry bytes x 8
+  d.low <<= k8;
+  d.range <<= k8;
+  d.cpos += k8 >> 3;
+  const bool rare = hi32(d.range) < 0x10000u;
+  if (__builtin_expect(__any(rare), 0)) {
+    if (rare) dec_rare(d);
+  }
+  const bool starve = (int)(d.fill - d.cpos) < 4;
+  if (__builtin_expect(__any(starve), 0)) {
+    if (starve) dec_sync(d);
+  }
+  dec_window(d);
   return s;
 }
 
@@ -387,11 +524,8 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   __syncthreads();
   const u32 k = blockIdx.x * WG + tid;
   if (k >= n_chunks) return;
-
-  RC_VGPR_FLOOR_96();
+  RC_VGPR_FLOOR_144();
   const u32 lane = tid & 63, wave = tid >> 6;
-  DecIO io;
-  io.ring = s_ring + wave * DEC_RING_ALLOC * 64 + lane;
 
   const u64 c0 = code_off[k];
   const u64 clen = code_len[k];
@@ -403,49 +537,45 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   }
   const uint8_t* cp = code + c0;
   const u32 a = (u32)((uintptr_t)cp & 15);
-  const uint8_t* gb = cp - a;
-  io.glast = (const uint8_t*)((uintptr_t)(cp + clen - 1) & ~(uintptr_t)15);
-  io.gnext = gb;
 
-  DecState st;
-  st.low = 0;
-  st.range = ~0ull;
-  st.flag = 0;
-  st.fill = 0;
-  st.cpos = a + 8;  // Decoder::new primes 8 bytes (decoder.rs:21)
-  st.lim = (u32)(clen < 0xFFFFFF00ull - a ? a + clen : 0xFFFFFF00ull);
-  io.pend = *reinterpret_cast<const uint4*>(io.gnext);
-  io.gnext = io.gnext < io.glast ? io.gnext + 16 : io.glast;
-  dec_refill_ready(st, io);
-  dec_window(st, io);
+  Dec d;
+  d.low = 0;
+  d.range = ~0ull;
+  d.err = 0;
+  d.fill = 0;
+  d.pend_ok = 0;
+  d.ring = s_ring + wave * DEC_RING_ALLOC * 64 + lane;
+  d.gnext = reinterpret_cast<const uint4*>(cp - a);
+  d.glast = reinterpret_cast<const uint4*>((uintptr_t)(cp + clen - 1) & ~(uintptr_t)15);
+  d.cpos = a + 8;  // Decoder::new primes 8 bytes (decoder.rs:21)
+  d.lim = (u32)(clen < 0xFFFFFF00ull - a ? a + clen : 0xFFFFFF00ull);
+  dec_issue(d);
+  dec_commit(d);
+  dec_issue(d);
+  dec_window(d);
 
   u64 i = 0;
   u64 head = (16 - ((uintptr_t)op & 15)) & 15;
   if (head > n) head = n;
-  for (; i < head; ++i) {
-    op[i] = (uint8_t)dec_symbol<DIV>(st, io, m, s_tab, s_lut);
-    dec_refill_ready(st, io);
-  }
-  const u64 nblk = (n - i) >> 4;
+  for (; i < head; ++i) op[i] = (uint8_t)dec_sym<DIV>(d, m, s_tab, s_lut);
+  // body: 16-symbol phases: store decoded block, commit pending load, maybe issue the next
+  const u64 nph = (n - i) >> 4;
   uint4* ob = reinterpret_cast<uint4*>(op + i);
-  for (u64 b = 0; b < nblk; ++b) {
+  for (u64 b = 0; b < nph; ++b) {
     u32 w[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[q] |= dec_symbol<DIV>(st, io, m, s_tab, s_lut) << (8 * j);
-      dec_refill_ready(st, io);
+      for (int j = 0; j < 4; ++j) w[q] |= dec_sym<DIV>(d, m, s_tab, s_lut) << (8 * j);
     }
     ob[b] = make_uint4(w[0], w[1], w[2], w[3]);
+    dec_phase(d);
   }
-  i += nblk << 4;
-  for (; i < n; ++i) {
-    op[i] = (uint8_t)dec_symbol<DIV>(st, io, m, s_tab, s_lut);
-    dec_refill_ready(st, io);
-  }
+  i += nph << 4;
+  for (; i < n; ++i) op[i] = (uint8_t)dec_sym<DIV>(d, m, s_tab, s_lut);
   // shift_left_buffer panics once more bytes are needed than the stream holds (decoder.rs:33)
-  if (!st.flag && st.cpos > st.lim) st.flag = RC_F_TRUNCATED;
-  flags[k] = st.flag;
+  if (!d.err && d.cpos > d.lim) d.err = RC_F_TRUNCATED;
+  flags[k] = d.err;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -731,8 +861,14 @@ rc_status rc_encode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
+#ifndef RC_EXTRA_LDS_ENC
+#define RC_EXTRA_LDS_ENC 0
+#endif
+#ifndef RC_EXTRA_LDS_DEC
+#define RC_EXTRA_LDS_DEC 0
+#endif
   if (m->div == DIV_POW2)
-    hipLaunchKernelGGL(k_encode_static<DIV_POW2>, grid, block, 0, ctx->cur, m->args, syms,
+    hipLaunchKernelGGL(k_encode_static<DIV_POW2>, grid, block, RC_EXTRA_LDS_ENC, ctx->cur, m->args, syms,
                        sym_off, n_chunks, out, out_off, out_len, flags);
   else
     hipLaunchKernelGGL(k_encode_static<DIV_MAGIC>, grid, block, 0, ctx->cur, m->args, syms,
@@ -751,7 +887,7 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   if (!g.ok) return RC_E_DEVICE;
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
   if (m->div == DIV_POW2)
-    hipLaunchKernelGGL(k_decode_static<DIV_POW2>, grid, block, 0, ctx->cur, m->args, code,
+    hipLaunchKernelGGL(k_decode_static<DIV_POW2>, grid, block, RC_EXTRA_LDS_DEC, ctx->cur, m->args, code,
                        code_off, code_len, syms_out, sym_off, n_chunks, flags);
   else
     hipLaunchKernelGGL(k_decode_static<DIV_MAGIC>, grid, block, 0, ctx->cur, m->args, code,
