@@ -31,7 +31,7 @@ typedef uint32_t u32;
 #define WAVES (WG / 64)
 #define ENC_RING 32          // dwords per lane in the encoder's output ring (128 B)
 #define DEC_RING 32          // dwords per lane in the decoder's input ring (128 B)
-#define DEC_RING_ALLOC 34    // + 2 mirror slots so a 12-byte window never wraps
+#define DEC_RING_ALLOC 36    // + 4 mirror slots so a 5-dword read never wraps
 #define LUT_BITS 12
 #define LUT_MAX_ENTRIES (1u << LUT_BITS)
 
@@ -43,8 +43,8 @@ enum { DIV_POW2 = 0, DIV_MAGIC = 1 };
 // register so its allocation is a multiple of 16; build() rejects any other count.
 #define RC_VGPR_FLOOR_96() asm volatile("; vgpr floor 96" ::: "v95")
 #define RC_VGPR_FLOOR_64() asm volatile("; vgpr floor 64" ::: "v63")
+#define RC_VGPR_FLOOR_112() asm volatile("; vgpr floor 112" ::: "v111")
 #define RC_VGPR_FLOOR_128() asm volatile("; vgpr floor 128" ::: "v127")
-#define RC_VGPR_FLOOR_144() asm volatile("; vgpr floor 144" ::: "v143")
 
 struct ModelArgs {
   const uint2* tab;  // [256] (cum, c); entries s >= n_symbols hold (0xFFFFFFFF, 0)
@@ -56,6 +56,7 @@ struct ModelArgs {
   u32 lut_shift;     // bucket = q >> lut_shift
   u32 lut_max;       // number of buckets - 1
   float ftotal;      // (float)total
+  u32 direct;        // 1: lut[q] = s | cum << 8 | c << 20 for every q < total (total <= 2048)
 };
 
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
@@ -69,6 +70,14 @@ static __device__ __forceinline__ u64 range_par_total(u64 range, const ModelArgs
   u64 q = __umul64hi(range, m.magic);  // q in {floor - 1, floor}
   u64 rem = range - q * (u64)m.total;
   return rem >= (u64)m.total ? q + 1 : q;
+}
+
+// r * v for the coder's products (range_coder.rs:65, :70).  SM (256 <= total <= 2^16): r < 2^56
+// and v <= 2^16, so the high half is a 24-bit multiply.
+template <int SM>
+static __device__ __forceinline__ u64 mul_rv(u64 r, u32 v) {
+  if (SM) return (u64)(u32)r * v + ((u64)__umul24(hi32(r), v) << 32);
+  return r * (u64)v;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -173,7 +182,7 @@ static __device__ __forceinline__ void enc_rare(Enc& e) {
 
 // Encoder::encode (encoder.rs:24-37) -> RangeCoder::param_update (range_coder.rs:53-92),
 // common path without branches.  Returns true when the lane needs enc_rare().
-template <int DIV>
+template <int DIV, int SM>
 static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, const uint2* s_tab,
                                                 u32 sym) {
   const uint2 t = s_tab[sym];
@@ -182,8 +191,8 @@ static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, cons
   e.err = (bad && e.err == 0) ? code : e.err;
   const u32 c = bad ? 1u : t.y, cum = bad ? 0u : t.x;
   const u64 r = range_par_total<DIV>(e.range, m);
-  e.range = r * (u64)c;   // range_coder.rs:65
-  e.low += r * (u64)cum;  // range_coder.rs:68-81 (overflow unreachable)
+  e.range = mul_rv<SM>(r, c);   // range_coder.rs:65
+  e.low += mul_rv<SM>(r, cum);  // range_coder.rs:68-81 (overflow unreachable)
   // no_carry_expansion in closed form: k = clz(low ^ upper) / 8 bytes settle (<= 3 here;
   // x == 0 means >= 4 and the rare path continues after these 3)
   const u32 x = hi32(e.low) ^ hi32(e.low + e.range);
@@ -201,12 +210,12 @@ static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, cons
 }
 
 // one symbol for the lanes with `act`; the rare path (wave-uniform branch) may flush
-template <int DIV>
+template <int DIV, int SM>
 static __device__ __forceinline__ void enc_sym(Enc& e, const ModelArgs& m, const uint2* s_tab,
                                                u32 sym, bool act, u32 lane, const u32* wring,
                                                const EncOut* wout) {
   bool rare = false;
-  if (act) rare = enc_step<DIV>(e, m, s_tab, sym);
+  if (act) rare = enc_step<DIV, SM>(e, m, s_tab, sym);
   if (__builtin_expect(__any((int)rare), 0)) {
     if (rare) enc_rare(e);
     enc_flush(e, lane, wring, wout);
@@ -214,40 +223,40 @@ static __device__ __forceinline__ void enc_sym(Enc& e, const ModelArgs& m, const
 }
 
 // 8 symbols from two dwords, then a flush check (wave-uniform)
-template <int DIV>
+template <int DIV, int SM>
 static __device__ __forceinline__ void enc8(Enc& e, const ModelArgs& m, const uint2* s_tab,
                                             u32 w0, u32 w1, bool act, u32 lane,
                                             const u32* wring, const EncOut* wout) {
-  enc_sym<DIV>(e, m, s_tab, w0 & 255u, act, lane, wring, wout);
-  enc_sym<DIV>(e, m, s_tab, (w0 >> 8) & 255u, act, lane, wring, wout);
-  enc_sym<DIV>(e, m, s_tab, (w0 >> 16) & 255u, act, lane, wring, wout);
-  enc_sym<DIV>(e, m, s_tab, w0 >> 24, act, lane, wring, wout);
-  enc_sym<DIV>(e, m, s_tab, w1 & 255u, act, lane, wring, wout);
-  enc_sym<DIV>(e, m, s_tab, (w1 >> 8) & 255u, act, lane, wring, wout);
-  enc_sym<DIV>(e, m, s_tab, (w1 >> 16) & 255u, act, lane, wring, wout);
-  enc_sym<DIV>(e, m, s_tab, w1 >> 24, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab, w0 & 255u, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab, (w0 >> 8) & 255u, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab, (w0 >> 16) & 255u, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab, w0 >> 24, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab, w1 & 255u, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab, (w1 >> 8) & 255u, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab, (w1 >> 16) & 255u, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab, w1 >> 24, act, lane, wring, wout);
   enc_flush(e, lane, wring, wout);
 }
 
-template <int DIV>
+template <int DIV, int SM>
 static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const uint2* s_tab,
                                              uint4 v, bool act, u32 lane, const u32* wring,
                                              const EncOut* wout) {
-  enc8<DIV>(e, m, s_tab, v.x, v.y, act, lane, wring, wout);
-  enc8<DIV>(e, m, s_tab, v.z, v.w, act, lane, wring, wout);
+  enc8<DIV, SM>(e, m, s_tab, v.x, v.y, act, lane, wring, wout);
+  enc8<DIV, SM>(e, m, s_tab, v.z, v.w, act, lane, wring, wout);
 }
 
 // one symbol fetched byte-wise (unaligned head / tail of a chunk)
-template <int DIV>
+template <int DIV, int SM>
 static __device__ __forceinline__ void enc_byte_sym(Enc& e, const ModelArgs& m,
                                                     const uint2* s_tab, const uint8_t* sp, u64 i,
                                                     bool act, u32 lane, const u32* wring,
                                                     const EncOut* wout) {
   const u32 sym = act ? (u32)sp[i] : 0u;
-  enc_sym<DIV>(e, m, s_tab, sym, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab, sym, act, lane, wring, wout);
 }
 
-template <int DIV>
+template <int DIV, int SM>
 __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint8_t* __restrict__ syms,
                                                         const u64* __restrict__ sym_off,
                                                         u32 n_chunks, uint8_t* __restrict__ out,
@@ -298,7 +307,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   const u64 tail0 = head + (ntile << 6);
   // head: byte-wise, all lanes in step (flush rounds are wave-wide)
   for (u64 i = 0; __any((int)(i < head)); ++i) {
-    enc_byte_sym<DIV>(e, m, s_tab, sp, i, i < head, lane, wring, wout);
+    enc_byte_sym<DIV, SM>(e, m, s_tab, sp, i, i < head, lane, wring, wout);
     if ((i & 7) == 7) enc_flush(e, lane, wring, wout);
   }
   // body: 64-symbol tiles, the next one prefetched
@@ -319,17 +328,17 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
       n2 = tp[(t + 1) * 4 + 2];
       n3 = tp[(t + 1) * 4 + 3];
     }
-    enc16<DIV>(e, m, s_tab, c0, act, lane, wring, wout);
-    enc16<DIV>(e, m, s_tab, c1, act, lane, wring, wout);
-    enc16<DIV>(e, m, s_tab, c2, act, lane, wring, wout);
-    enc16<DIV>(e, m, s_tab, c3, act, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c0, act, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c1, act, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c2, act, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c3, act, lane, wring, wout);
     c0 = n0;
     c1 = n1;
     c2 = n2;
     c3 = n3;
   }
   for (u64 j = 0; __any((int)(tail0 + j < n)); ++j) {  // j is wave-uniform
-    enc_byte_sym<DIV>(e, m, s_tab, sp, tail0 + j, tail0 + j < n, lane, wring, wout);
+    enc_byte_sym<DIV, SM>(e, m, s_tab, sp, tail0 + j, tail0 + j < n, lane, wring, wout);
     if ((j & 7) == 7) enc_flush(e, lane, wring, wout);
   }
 
@@ -402,6 +411,8 @@ static __device__ __forceinline__ void dec_commit(Dec& d) {
   if (j == 0) {  // mirror slots
     rp[DEC_RING * 64] = d.pend[0].x;
     rp[(DEC_RING + 1) * 64] = d.pend[0].y;
+    rp[(DEC_RING + 2) * 64] = d.pend[0].z;
+    rp[(DEC_RING + 3) * 64] = d.pend[0].w;
   }
   d.fill += 64;
   d.pend_ok = 0;
@@ -462,29 +473,50 @@ static __device__ __forceinline__ void dec_fix(u32& s, uint2& t, u64& A, u64& B,
   }
 }
 
-// Decoder::decode (decoder.rs:38-54) with FreqTable::find_index (sample_impl.rs:27-45)
-template <int DIV>
+// Decoder::decode (decoder.rs:38-54) with FreqTable::find_index (sample_impl.rs:27-45).
+// SM: 256 <= total <= 2^16 (then range >= 2^32 after narrowing, so at most 3 bytes settle).
+// u32 -> f32 as the single instruction; written out because hipcc otherwise widens a
+// (float)hi32(v) back into its multi-instruction u64 -> f32 sequence
+static __device__ __forceinline__ float cvt_f32(u32 v) {
+  float f;
+  asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"(v));
+  return f;
+}
+
+template <int DIV, int SM, int LUT>
 static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const uint2* s_tab,
                                               const u32* s_lut) {
+  // speculative read of the next window: bytes [cpos - 8, cpos - 8 + 16 (+4)) cover any
+  // common-path consumption (<= 3 bytes, <= 7 when !SM)
+  const u32 p0 = d.cpos - 8;
+  const u32* rp = d.ring + ((p0 >> 2) & (DEC_RING - 1)) * 64;
+  const u32 D0 = rp[0], D1 = rp[64], D2 = rp[128], D3 = rp[192];
+  const u32 D4 = SM ? 0u : rp[256];
   const u64 x = d.data - d.low;
   const u64 r = range_par_total<DIV>(d.range, m);
-  // hint q ~ x / r (relative error ~2^-22): bucket table -> candidate symbol
-  // (opaque halves: keeps hipcc from re-fusing this into an exact u64->f32 conversion)
-  u32 xh = hi32(x), xl = (u32)x, rh = hi32(r), rl = (u32)r;
-  asm volatile("" : "+v"(xh), "+v"(xl), "+v"(rh), "+v"(rl));
-  const float fx = fmaf((float)xh, 4294967296.0f, (float)xl);
-  const float fr = fmaf((float)rh, 4294967296.0f, (float)rl);
-  const float qf = fminf(fx * __builtin_amdgcn_rcpf(fr), 4.0e9f);
+  // hint q ~ x / r ~ x * total / range from the top 32 bits of x and range, both shifted by
+  // clz(range) (range >= 2^48, so the shift is < 16); relative error ~2^-22
+  const u32 e = (u32)__builtin_clz(hi32(d.range));
+  const float X = cvt_f32(hi32(x << e)), R = cvt_f32(hi32(d.range << e));
+  const float qf = fminf(X * (m.ftotal * __builtin_amdgcn_rcpf(R)), 4.0e9f);
   const u32 qh = (u32)qf;
-  const u32 b = min(qh >> m.lut_shift, m.lut_max);
-  const u32 ent = s_lut[b];
-  u32 s = ((qh - (b << m.lut_shift)) >= (ent >> 16)) ? ((ent >> 8) & 255u) : (ent & 255u);
-  uint2 t = s_tab[s];
-  u64 A = r * (u64)t.x;
-  u64 B = r * (u64)t.y;
+  u32 s;
+  uint2 t;
+  if (LUT) {  // direct table: candidate symbol and its (cum, c) in one LDS read
+    const u32 ent = s_lut[min(qh, m.total - 1)];
+    s = ent & 255u;
+    t = make_uint2((ent >> 8) & 0xFFFu, ent >> 20);
+  } else {  // bucket table, then the (cum, c) table
+    const u32 b = min(qh >> m.lut_shift, m.lut_max);
+    const u32 ent = s_lut[b];
+    s = ((qh - (b << m.lut_shift)) >= (ent >> 16)) ? ((ent >> 8) & 255u) : (ent & 255u);
+    t = s_tab[s];
+  }
+  u64 A = mul_rv<SM>(r, t.x);
+  u64 B = mul_rv<SM>(r, t.y);
   // exact verification r*cum[s] <= x < r*cum[s+1]; the hint is rarely off
   const bool off = (A > x) | ((s + 1 < m.n) & (x - A >= B));
-  if (__builtin_expect(__any(off), 0)) {
+  if (__builtin_expect(__any((int)off), 0)) {
     if (off) dec_fix(s, t, A, B, x, r, s_tab, m.n);
   }
   if (t.y == 0) {  // only on corrupt input (reference: endless loop); an over-read came first
@@ -494,37 +526,49 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   // param_update (range_coder.rs:53-92)
   d.low += A;
   d.range = B;
-  const u32 k8 = (u32)__clzll(d.low ^ (d.low + d.range)) & 56u;  // no-carry bytes x 8
+  const u64 xx = d.low ^ (d.low + d.range);
+  const u32 k8 = SM ? ((u32)__builtin_clz(hi32(xx)) & 24u) : ((u32)__clzll(xx) & 56u);
   d.low <<= k8;
   d.range <<= k8;
-  d.cpos += k8 >> 3;
-  const bool rare = hi32(d.range) < 0x10000u;
-  if (__builtin_expect(__any(rare), 0)) {
-    if (rare) dec_rare(d);
+  const u32 kb = k8 >> 3;
+  d.cpos += kb;
+  // next window from the speculative read
+  const u32 o = (p0 & 3) + kb;  // byte offset of the new window in D0..D4
+  const u32 i = o >> 2, sh = o & 3;
+  const u32 Da = SM ? (i ? D1 : D0) : (i == 0 ? D0 : i == 1 ? D1 : D2);
+  const u32 Db = SM ? (i ? D2 : D1) : (i == 0 ? D1 : i == 1 ? D2 : D3);
+  const u32 Dc = SM ? (i ? D3 : D2) : (i == 0 ? D2 : i == 1 ? D3 : D4);
+  const u32 w0 = __builtin_amdgcn_alignbyte(Db, Da, sh);
+  const u32 w1 = __builtin_amdgcn_alignbyte(Dc, Db, sh);
+  d.data = ((u64)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
+  // rare: range_reduction_expansion, or the ring ran short -> re-read the window
+  const bool rare = (hi32(d.range) < 0x10000u) | ((int)(d.fill - d.cpos) < 4);
+  if (__builtin_expect(__any((int)rare), 0)) {
+    if (rare) {
+      dec_rare(d);
+      if ((int)(d.fill - d.cpos) < 4) dec_sync(d);
+      dec_window(d);
+    }
   }
-  const bool starve = (int)(d.fill - d.cpos) < 4;
-  if (__builtin_expect(__any(starve), 0)) {
-    if (starve) dec_sync(d);
-  }
-  dec_window(d);
   return s;
 }
 
-template <int DIV>
+template <int DIV, int SM, int LUT>
 __global__ __launch_bounds__(WG) void k_decode_static(
     ModelArgs m, const uint8_t* __restrict__ code, const u64* __restrict__ code_off,
     const u64* __restrict__ code_len, uint8_t* __restrict__ syms_out,
     const u64* __restrict__ sym_off, u32 n_chunks, u32* __restrict__ flags) {
   __shared__ uint2 s_tab[256];
-  __shared__ u32 s_lut[LUT_MAX_ENTRIES];
   __shared__ u32 s_ring[WAVES * DEC_RING_ALLOC * 64];
+  extern __shared__ u32 s_lut[];  // lut_max + 1 entries, sized at launch: the WG's LDS
+                                  // footprint sets how many WGs share a CU
   const u32 tid = threadIdx.x;
   s_tab[tid] = m.tab[tid];
   for (u32 j = tid; j <= m.lut_max; j += WG) s_lut[j] = m.lut[j];
   __syncthreads();
   const u32 k = blockIdx.x * WG + tid;
   if (k >= n_chunks) return;
-  RC_VGPR_FLOOR_144();
+  RC_VGPR_FLOOR_112();
   const u32 lane = tid & 63, wave = tid >> 6;
 
   const u64 c0 = code_off[k];
@@ -557,7 +601,7 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   u64 i = 0;
   u64 head = (16 - ((uintptr_t)op & 15)) & 15;
   if (head > n) head = n;
-  for (; i < head; ++i) op[i] = (uint8_t)dec_sym<DIV>(d, m, s_tab, s_lut);
+  for (; i < head; ++i) op[i] = (uint8_t)dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut);
   // body: 16-symbol phases: store decoded block, commit pending load, maybe issue the next
   const u64 nph = (n - i) >> 4;
   uint4* ob = reinterpret_cast<uint4*>(op + i);
@@ -566,13 +610,13 @@ __global__ __launch_bounds__(WG) void k_decode_static(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[q] |= dec_sym<DIV>(d, m, s_tab, s_lut) << (8 * j);
+      for (int j = 0; j < 4; ++j) w[q] |= dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut) << (8 * j);
     }
     ob[b] = make_uint4(w[0], w[1], w[2], w[3]);
     dec_phase(d);
   }
   i += nph << 4;
-  for (; i < n; ++i) op[i] = (uint8_t)dec_sym<DIV>(d, m, s_tab, s_lut);
+  for (; i < n; ++i) op[i] = (uint8_t)dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut);
   // shift_left_buffer panics once more bytes are needed than the stream holds (decoder.rs:33)
   if (!d.err && d.cpos > d.lim) d.err = RC_F_TRUNCATED;
   flags[k] = d.err;
@@ -808,6 +852,17 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
     lut[b] = s | (s1 << 8) | (split << 16);
   }
 
+  if (total_freq <= 2048) {  // direct table: q -> s | cum << 8 | c << 20
+    a.direct = 1;
+    a.lut_shift = 0;
+    a.lut_max = total_freq - 1;
+    lut.assign(total_freq, 0);
+    u32 sym = 0;
+    for (u32 q = 0; q < total_freq; ++q) {
+      while (sym + 1 < n_symbols && cum_freq[sym + 1] <= q) ++sym;
+      lut[q] = sym | (cum_freq[sym] << 8) | (c_freq[sym] << 20);
+    }
+  }
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
   const size_t tab_bytes = 256 * sizeof(uint2);
@@ -861,18 +916,16 @@ rc_status rc_encode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
-#ifndef RC_EXTRA_LDS_ENC
-#define RC_EXTRA_LDS_ENC 0
-#endif
-#ifndef RC_EXTRA_LDS_DEC
-#define RC_EXTRA_LDS_DEC 0
-#endif
-  if (m->div == DIV_POW2)
-    hipLaunchKernelGGL(k_encode_static<DIV_POW2>, grid, block, RC_EXTRA_LDS_ENC, ctx->cur, m->args, syms,
-                       sym_off, n_chunks, out, out_off, out_len, flags);
-  else
-    hipLaunchKernelGGL(k_encode_static<DIV_MAGIC>, grid, block, 0, ctx->cur, m->args, syms,
-                       sym_off, n_chunks, out, out_off, out_len, flags);
+  const bool sm = m->args.total >= 256 && m->args.total <= 65536;
+#define RC_ENC_LAUNCH(D, S)                                                                \
+  hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, ctx->cur, m->args, syms,    \
+                     sym_off, n_chunks, out, out_off, out_len, flags)
+  if (m->div == DIV_POW2) {
+    if (sm) RC_ENC_LAUNCH(DIV_POW2, 1); else RC_ENC_LAUNCH(DIV_POW2, 0);
+  } else {
+    if (sm) RC_ENC_LAUNCH(DIV_MAGIC, 1); else RC_ENC_LAUNCH(DIV_MAGIC, 0);
+  }
+#undef RC_ENC_LAUNCH
   return launch_status();
 }
 
@@ -886,12 +939,20 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
-  if (m->div == DIV_POW2)
-    hipLaunchKernelGGL(k_decode_static<DIV_POW2>, grid, block, RC_EXTRA_LDS_DEC, ctx->cur, m->args, code,
-                       code_off, code_len, syms_out, sym_off, n_chunks, flags);
-  else
-    hipLaunchKernelGGL(k_decode_static<DIV_MAGIC>, grid, block, 0, ctx->cur, m->args, code,
-                       code_off, code_len, syms_out, sym_off, n_chunks, flags);
+  const bool sm = m->args.total >= 256 && m->args.total <= 65536;
+#define RC_DEC_LAUNCH(D, S, L)                                                             \
+  hipLaunchKernelGGL((k_decode_static<D, S, L>), grid, block, lut_bytes, ctx->cur, m->args, \
+                     code, code_off, code_len, syms_out, sym_off, n_chunks, flags)
+  const bool dl = m->args.direct != 0;
+  const size_t lut_bytes = (size_t)(m->args.lut_max + 1) * sizeof(u32);
+  if (m->div == DIV_POW2) {
+    if (sm) { if (dl) RC_DEC_LAUNCH(DIV_POW2, 1, 1); else RC_DEC_LAUNCH(DIV_POW2, 1, 0); }
+    else    { if (dl) RC_DEC_LAUNCH(DIV_POW2, 0, 1); else RC_DEC_LAUNCH(DIV_POW2, 0, 0); }
+  } else {
+    if (sm) { if (dl) RC_DEC_LAUNCH(DIV_MAGIC, 1, 1); else RC_DEC_LAUNCH(DIV_MAGIC, 1, 0); }
+    else    { if (dl) RC_DEC_LAUNCH(DIV_MAGIC, 0, 1); else RC_DEC_LAUNCH(DIV_MAGIC, 0, 0); }
+  }
+#undef RC_DEC_LAUNCH
   return launch_status();
 }
 
