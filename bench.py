@@ -8,8 +8,11 @@ PModel (c[i] = 1, total 256), synthetic symbols generated in HBM.  One step = en
 value = symbols round-tripped / second over all ranks = N_sym / (t_enc + t_dec), Gsymbols/s.
 
 N > 1 (torchrun, one process per GPU): every rank codes its own 2^20 chunks (chunks are
-independent streams — no data-path collective; weak scaling).  The torch.distributed process
-group (RCCL) is used only for the barrier and the max-over-ranks of the timed region.
+independent streams — no data-path collective; weak scaling): rank r holds global chunks
+[r * 2^20, (r + 1) * 2^20) of one synthetic stream.  With --global-chunks G the G chunks are
+sharded instead (configs[4]: a fixed stream split over the GPUs; strong scaling).  The
+torch.distributed process group (RCCL) is used only for the barrier and the max-over-ranks of
+the timed region (range_coder_rust_amd/shard.py).
 
 Also reported: the Zipf(1.2) configuration (configs[2]) on the same buffers, per-kernel times,
 the HBM roofline of the dominant kernel and a CPU baseline (the C oracle on the host cores,
@@ -36,6 +39,8 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU")
+    p.add_argument("--global-chunks", type=int, default=0,
+                   help="shard this many chunks over the ranks instead (strong scaling)")
     p.add_argument("--chunk-bytes", type=int, default=65536)
     p.add_argument("--config", choices=["uniform", "zipf"], default="uniform")
     p.add_argument("--no-zipf", action="store_true", help="skip the secondary Zipf leg")
@@ -55,7 +60,7 @@ def table(cfg):
 class Leg:
     """One configuration resident in HBM: inputs, code slots, decoded output."""
 
-    def __init__(self, torch, rc, synth, ctx, cfg, n, L, rank, bufs=None):
+    def __init__(self, torch, rc, synth, ctx, cfg, n, L, first_chunk, bufs=None):
         c, cum, total = table(cfg)
         self.cfg, self.n, self.L = cfg, n, L
         self.model = rc.StaticModel(c, cum, total, ctx=ctx)
@@ -70,7 +75,8 @@ class Leg:
         self.bufs = bufs
         self.syms, self.out, self.dec = bufs["syms"], bufs["out"], bufs["dec"]
         self.inv = synth.inverse_cdf(c)
-        self.seed = SEED ^ (rank << 40)
+        from range_coder_rust_amd import shard
+        self.seed = shard.synth_seed(SEED, first_chunk)  # this rank's slice of one global stream
         synth.fill(ctx, self.seed, self.inv, self.syms, L, n)
         self.sym_off = torch.arange(n + 1, dtype=torch.int64, device=dev) * L
         self.out_off = torch.arange(n + 1, dtype=torch.int64, device=dev) * cap
@@ -124,10 +130,8 @@ def run_leg(torch, dist, leg, steps, warmup, world):
     t = time.perf_counter() - t0
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
-    if world > 1:
-        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
+    from range_coder_rust_amd import shard
+    t = shard.max_over_ranks(t, dist if world > 1 else None, device="cuda")
     # correctness of the timed work: no chunk flagged, decode(encode(x)) == x
     ok = (int(leg.fenc.abs().sum()) == 0 and int(leg.fdec.abs().sum()) == 0
           and equal_chunked(torch, leg.dec, leg.syms))
@@ -187,10 +191,17 @@ def main():
     from range_coder_rust_amd import synth
     ctx = rc.default_context(local)
 
-    n, L = args.chunks, args.chunk_bytes
-    leg = Leg(torch, rc, synth, ctx, args.config, n, L, rank)
+    from range_coder_rust_amd import shard
+    L = args.chunk_bytes
+    if args.global_chunks:
+        lo, hi = shard.shard_range(args.global_chunks, world, rank)
+        n, n_all, scaling = hi - lo, args.global_chunks, "strong"
+    else:
+        n = args.chunks
+        lo, n_all, scaling = rank * n, n * world, "weak"
+    leg = Leg(torch, rc, synth, ctx, args.config, n, L, lo)
     res = run_leg(torch, dist, leg, args.steps, args.warmup, world)
-    n_sym_all = n * L * world
+    n_sym_all = n_all * L
     value = n_sym_all * args.steps / res["t"] / 1e9
 
     # algorithmic bytes per launch: encode reads N symbols + writes the code, decode reads the
@@ -219,7 +230,7 @@ def main():
 
     extras = {}
     if not args.no_zipf and args.config == "uniform":
-        z = Leg(torch, rc, synth, ctx, "zipf", n, L, rank, bufs=leg.bufs)
+        z = Leg(torch, rc, synth, ctx, "zipf", n, L, lo, bufs=leg.bufs)
         zr = run_leg(torch, dist, z, max(2, args.steps // 2), 1, world)
         zb = n * L + zr["code_bytes"]
         extras["zipf1.2"] = dict(
@@ -242,6 +253,11 @@ def main():
         cpu_b = cpu_baseline(torch, leg, args.cpu_seconds, threads)
 
     if rank == 0:
+        model = ("uniform-256 static (c=1, total=256)" if args.config == "uniform"
+                 else "Zipf(1.2) static (total 2^16)")
+        shape = (f"configs[4]: {n_all} x {L // 1024} KiB chunks sharded over {world} GPU(s)"
+                 if args.global_chunks else f"configs[1]: {n} x {L // 1024} KiB chunks per GPU")
+        workload = f"{shape}, {model}, encode then decode, inputs resident in HBM"
         line = {
             "metric": "Gsymbols/s encode+decode, 256-sym static model, 64KiB chunks, 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -251,14 +267,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(res["t"] / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic",
-            "config": {"workload": f"configs[1]: {n} x {L // 1024} KiB chunks per GPU, "
-                                   f"{'uniform-256 static (c=1, total=256)' if args.config == 'uniform' else 'Zipf(1.2) static (total 2^16)'}, "
-                                   "encode then decode, inputs resident in HBM",
-                       "chunks_per_gpu": n, "chunk_symbols": L, "alphabet": 256,
+            "config": {"workload": workload,
+                       "chunks_per_gpu": n, "chunks_total": n_all, "chunk_symbols": L,
+                       "alphabet": 256,
                        "total_freq": int(leg.total), "parallelism": f"chunk-shard x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu_b,

@@ -6,17 +6,19 @@
 // range_reduction_expansion :126-135), src/encoder.rs (encode :24-37, finish :40-46) and
 // src/decoder.rs (new :14-23, decode :38-54) bit-exactly, with these MI355X-specific choices:
 //  * coder state (lower_bound, range, decoder data window) lives in VGPR pairs;
-//  * the PModel snapshot (cum, c) and the decoder's inverse-CDF bucket table live in LDS;
+//  * the PModel snapshot (cum, c) and the decoder's inverse-CDF table live in LDS;
 //  * the no-carry loop (range_coder.rs:83-85) is evaluated in closed form: it settles exactly
 //    k = clz64(low ^ (low + range)) / 8 bytes (proof in DESIGN.md §3), so the wave does not
 //    diverge on it;
 //  * range / total (range_coder.rs:38-40) is a shift for power-of-two totals and an exact
 //    multiply-high by a host-computed reciprocal otherwise (no 64-bit divide on the VALU);
 //  * the decoder's find_index division + binary search (sample_impl.rs:27-45) is replaced by a
-//    float hint -> LDS bucket table -> exact integer verification r*cum[s] <= data-low <
+//    float hint -> LDS inverse-CDF table -> exact integer verification r*cum[s] <= data-low <
 //    r*cum[s+1], which yields the same index for every input, valid or corrupt;
-//  * input symbols are read 16 B per lane per load, output bytes are staged through a per-lane
-//    LDS ring and written back 16 B per lane per store.
+//  * encoder: symbols are read 64 B per lane per tile; settled bytes go through a per-lane LDS
+//    ring and are written by cooperative flush rounds, 16 chunks x 64 B per store instruction;
+//  * decoder: the code is read 64 B per lane into a per-lane LDS ring one 16-symbol phase
+//    ahead; decoded symbols are written 16 B per lane per phase.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -367,8 +369,8 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
 // ------------------------------------------------------------------------------------------
 // Decoder
 //
-// Per lane: one chunk.  The code stream is staged through a per-lane 128-B LDS ring (+2
-// mirror dwords so a 12-byte window never wraps), refilled 64 B at a time: at each 16-symbol
+// Per lane: one chunk.  The code stream is staged through a per-lane 128-B LDS ring (+4
+// mirror dwords so a 20-byte window never wraps), refilled 64 B at a time: at each 16-symbol
 // phase boundary a lane stores its 16 decoded symbols, moves its pending 64-B load into the
 // ring and, if the ring has room, issues the next 64-B load.  The pending load is therefore
 // waited for with vmcnt(1) one phase after it was issued.  Lanes that consume faster than the

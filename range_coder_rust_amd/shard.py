@@ -1,0 +1,64 @@
+"""Chunk sharding across GPUs: one process per GPU, contiguous chunk ranges.
+
+Every chunk is an independent stream (a fresh reference Encoder per chunk, encoder.rs:14-16),
+so a batch splits across ranks with no data-path collective.  The only cross-rank
+bookkeeping is control data: where each rank's code lands in a global arena (an exclusive
+scan of per-rank byte counts, one int64 per rank) and the max-over-ranks step time.
+"""
+import numpy as np
+
+from .synth import GOLDEN
+
+M64 = (1 << 64) - 1
+
+
+def shard_range(n_chunks, world, rank):
+    """[lo, hi) of the global chunks owned by `rank`: contiguous, sizes differ by at most one
+    (the first n_chunks % world ranks take one more)."""
+    if world < 1 or not 0 <= rank < world or n_chunks < 0:
+        raise ValueError(f"bad shard: n_chunks={n_chunks} world={world} rank={rank}")
+    q, r = divmod(n_chunks, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def synth_seed(seed, first_chunk):
+    """Seed under which rc_synth_fill's chunk 0 is global chunk `first_chunk` of `seed`.
+
+    Symbol i of chunk k is drawn from mix64(seed + GOLDEN * ((k << 32) + i/4 + 1)), so shifting
+    k by `first_chunk` is adding GOLDEN * (first_chunk << 32) to the seed (mod 2^64): every
+    rank then generates exactly its slice of one global stream, whatever the world size."""
+    return (seed + GOLDEN * ((first_chunk << 32) & M64)) & M64
+
+
+def exclusive_scan(counts):
+    """Exclusive prefix sum (u64) of per-chunk or per-rank byte counts, plus the total."""
+    c = np.asarray(counts, dtype=np.uint64)
+    off = np.zeros(c.size + 1, dtype=np.uint64)
+    np.cumsum(c, out=off[1:])
+    return off[:-1], int(off[-1])
+
+
+def global_code_offset(local_bytes, dist=None, device=None):
+    """(base, total): where this rank's code starts in the concatenation of all ranks' code,
+    in rank order, and the global code size.  Single process: (0, local_bytes)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return 0, int(local_bytes)
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    t = torch.tensor([int(local_bytes)], dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    per_rank = [int(x.item()) for x in out]
+    off, total = exclusive_scan(per_rank)
+    return int(off[rank]), total
+
+
+def max_over_ranks(value, dist=None, device=None):
+    """The slowest rank's value (bench timing: the job ends when the last rank ends)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(value)
+    import torch
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -229,6 +229,38 @@ def test_error_flags_gpu(ctx):
         rc.StaticModel([1, 2], [0, 2], 3)  # cum[1] != cum[0] + c[0]
 
 
+def test_bad_models_rejected_by_abi(ctx):
+    """rc_model_create_static validates the PModel snapshot itself (not only the Python layer)."""
+    import ctypes
+    N = rc.api.N
+    lib = N.load()
+
+    def create(c, cum, total, n=None):
+        c = np.ascontiguousarray(c, np.uint32)
+        cum = np.ascontiguousarray(cum, np.uint32)
+        h = ctypes.c_void_p()
+        st = lib.rc_model_create_static(ctx.handle, len(c) if n is None else n,
+                                        c.ctypes.data_as(ctypes.c_void_p),
+                                        cum.ctypes.data_as(ctypes.c_void_p), total,
+                                        ctypes.byref(h))
+        if st == N.RC_OK:
+            assert lib.rc_model_destroy(h) == N.RC_OK
+        else:
+            assert h.value is None
+        return st
+
+    assert create([1, 5, 2], [0, 1, 6], 8) == N.RC_OK
+    assert create([0, 3], [0, 0], 3) == N.RC_OK  # zero-frequency symbols are allowed
+    assert create([1, 5, 2], [1, 2, 7], 8) == N.RC_E_BAD_MODEL  # cum[0] != 0
+    assert create([1, 5, 2], [0, 1, 7], 8) == N.RC_E_BAD_MODEL  # cum not the prefix sum
+    assert create([1, 5, 2], [0, 1, 6], 9) == N.RC_E_BAD_MODEL  # total != sum(c)
+    assert create([0, 0], [0, 0], 0) == N.RC_E_BAD_MODEL  # total 0
+    assert create([1] * 257, np.arange(257), 257) == N.RC_E_BAD_MODEL  # alphabet > 256
+    assert create([1], [0], 1, n=0) == N.RC_E_BAD_MODEL
+    big = [0xFFFFFFFF, 1]  # sum overflows u32: rejected, not wrapped
+    assert create(big, [0, 0xFFFFFFFF], 0) == N.RC_E_BAD_MODEL
+
+
 def test_synth_matches_host(ctx):
     for (c, _, _), L in ((synth.uniform_table(), 4096), (synth.zipf_table(), 1000)):
         inv = synth.inverse_cdf(c)
