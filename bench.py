@@ -44,6 +44,7 @@ def parse():
     p.add_argument("--chunk-bytes", type=int, default=65536)
     p.add_argument("--config", choices=["uniform", "zipf"], default="uniform")
     p.add_argument("--no-zipf", action="store_true", help="skip the secondary Zipf leg")
+    p.add_argument("--no-adaptive", action="store_true", help="skip the adaptive (C4) leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU sample wall time")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
@@ -53,6 +54,7 @@ def parse():
 
 
 def table(cfg):
+    """The static model of cfg, or for "adaptive" the Zipf table its data is drawn from."""
     from range_coder_rust_amd import synth
     return synth.uniform_table() if cfg == "uniform" else synth.zipf_table()
 
@@ -63,10 +65,14 @@ class Leg:
     def __init__(self, torch, rc, synth, ctx, cfg, n, L, first_chunk, bufs=None):
         c, cum, total = table(cfg)
         self.cfg, self.n, self.L = cfg, n, L
-        self.model = rc.StaticModel(c, cum, total, ctx=ctx)
+        if cfg == "adaptive":  # configs[3]: the C4 model over Zipf(1.2) data
+            self.model = rc.AdaptiveModel(256, **rc.ADAPTIVE_DEFAULTS, ctx=ctx)
+            cap = rc.slot_capacity(L, 6.0, slack=1.02)  # Zipf(1.2) codes at ~5.4 bits/symbol
+        else:
+            self.model = rc.StaticModel(c, cum, total, ctx=ctx)
+            cap = rc.slot_capacity(L, 8.0, slack=1.02)  # >= the uniform model's 8 bits/symbol
         self.c, self.cum, self.total = c, cum, total
         dev = torch.device("cuda", ctx.device)
-        cap = rc.slot_capacity(L, 8.0, slack=1.02)  # >= the uniform model's 8 bits/symbol
         self.cap = cap
         if bufs is None:
             bufs = dict(syms=torch.empty(n * L, dtype=torch.uint8, device=dev),
@@ -242,6 +248,21 @@ def main():
             roofline_frac_encode=round(zb / zr["enc_ms"] / 1e6 / HBM_PEAK_GBPS, 4),
             roofline_frac_decode=round(zb / zr["dec_ms"] / 1e6 / HBM_PEAK_GBPS, 4),
             bit_exact_round_trip=zr["ok"])
+    if not args.no_adaptive and args.config == "uniform" and L % 16384 == 0:
+        La = 16384
+        na = n * (L // La)
+        a = Leg(torch, rc, synth, ctx, "adaptive", na, La, lo * (L // La), bufs=leg.bufs)
+        ar = run_leg(torch, dist, a, max(2, args.steps // 2), 1, world)
+        extras["adaptive_c4"] = dict(
+            workload=f"configs[3]: {na} x 16 KiB chunks per GPU, adaptive order-0 "
+                     f"(increment 32, limit 57343, period 256) over Zipf(1.2) data",
+            value=round(n_all * L * max(2, args.steps // 2) / ar["t"] / 1e9, 3),
+            encode_gsym_s=round(na * La / ar["enc_ms"] / 1e6, 3),
+            decode_gsym_s=round(na * La / ar["dec_ms"] / 1e6, 3),
+            encode_ms=round(ar["enc_ms"], 3), decode_ms=round(ar["dec_ms"], 3),
+            bytes_per_symbol=round(ar["code_bytes"] / (na * La), 5),
+            bit_exact_round_trip=ar["ok"])
+    if extras:
         # restore the headline inputs for the CPU baseline sample
         synth.fill(ctx, leg.seed, leg.inv, leg.syms, L, n)
         leg.encode()

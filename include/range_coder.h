@@ -84,11 +84,16 @@ rc_status rc_device_info(int device, char* buf, size_t buf_len);
 rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t* c_freq_host,
                                  const uint32_t* cum_freq_host, uint32_t total_freq,
                                  rc_model** out);
-/* Adaptive order-0 model (build-defined; the reference ships none):
- * per chunk, c[i] = 1 for i < n_symbols; after coding symbol s: c[s] += increment, and when the
- * total exceeds limit every c[i] = (c[i] + 1) >> 1.  Requires limit + increment < 2^31.     */
+/* Adaptive order-0 model (build-defined; the reference ships none).
+ * Per chunk, c[i] = 1 for i < n_symbols.  After coding the i-th symbol s (0-based):
+ * c[s] += increment, and if (i + 1) % period == 0 and the total exceeds limit, every
+ * c[i] = (c[i] + 1) >> 1.  The coder sees (c[s], cum[s], total) before the update.
+ * Accepted when 1 <= n_symbols <= 256, increment >= 1, period is a power of two <= 65536 and
+ * n_symbols + increment*period <= limit <= 65535 - increment*period (so the total, and every
+ * count, stays below 2^16 for all inputs).  Default (config C4): increment 32, limit 57343,
+ * period 256.                                                                               */
 rc_status rc_model_create_adaptive(rc_ctx* ctx, uint32_t n_symbols, uint32_t increment,
-                                   uint32_t limit, rc_model** out);
+                                   uint32_t limit, uint32_t period, rc_model** out);
 rc_status rc_model_destroy(rc_model* m);
 
 /* ---- batch encode (replaces n_chunks x {Encoder::new; encode...; finish}) ----

@@ -42,9 +42,10 @@ def lib():
         L.orc_encode_batch.restype = None
         L.orc_decode_batch.argtypes = [_P, _P, _U32, _U32, _P, _P, _P, _P, _P, _U32, _P, ctypes.c_int]
         L.orc_decode_batch.restype = None
-        L.orc_encode_adaptive.argtypes = [_U32, _U32, _U32, _P, _U64, _P, _U64, ctypes.POINTER(_U64)]
+        L.orc_encode_adaptive.argtypes = [_U32, _U32, _U32, _U32, _P, _U64, _P, _U64,
+                                          ctypes.POINTER(_U64)]
         L.orc_encode_adaptive.restype = _U32
-        L.orc_decode_adaptive.argtypes = [_U32, _U32, _U32, _P, _U64, _U64, _P]
+        L.orc_decode_adaptive.argtypes = [_U32, _U32, _U32, _U32, _P, _U64, _U64, _P]
         L.orc_decode_adaptive.restype = _U32
         L.orc_fnv1a64.argtypes = [_P, _U64]
         L.orc_fnv1a64.restype = _U64
@@ -117,21 +118,22 @@ def decode_batch(c, cum, total, code, code_off, code_len, sym_off, threads=1):
     return out[: int(sym_off[-1])], flags[:n]
 
 
-def encode_adaptive(n_alpha, inc, limit, syms, cap=None):
+def encode_adaptive(n_alpha, inc, limit, period, syms, cap=None):
     s = _u8(syms)
     if cap is None:
         cap = 16 * len(s) + 64
     out = np.zeros(max(cap, 1), np.uint8)
     ol = _U64()
-    f = lib().orc_encode_adaptive(n_alpha, inc, limit, _ptr(s), len(s), _ptr(out), cap,
+    f = lib().orc_encode_adaptive(n_alpha, inc, limit, period, _ptr(s), len(s), _ptr(out), cap,
                                   ctypes.byref(ol))
     return int(f), bytes(out[: min(ol.value, cap)]), int(ol.value)
 
 
-def decode_adaptive(n_alpha, inc, limit, code, n):
+def decode_adaptive(n_alpha, inc, limit, period, code, n):
     code = _u8(code)
     out = np.zeros(max(n, 1), np.uint8)
-    f = lib().orc_decode_adaptive(n_alpha, inc, limit, _ptr(code), len(code), n, _ptr(out))
+    f = lib().orc_decode_adaptive(n_alpha, inc, limit, period, _ptr(code), len(code), n,
+                                  _ptr(out))
     return int(f), out[:n]
 
 

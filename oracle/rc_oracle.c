@@ -117,17 +117,20 @@ static void adapt_init(adapt_model* m, uint32_t n) {
     m->total = m->cum[n];
 }
 
-static void adapt_update(adapt_model* m, uint32_t s, uint32_t inc, uint32_t limit) {
+/* after coding symbol number i (0-based) of the chunk: c[s] += inc; then, every period-th
+ * symbol, halve all counts (rounding up) if the total exceeds limit */
+static void adapt_update(adapt_model* m, uint32_t s, uint32_t inc, uint32_t limit,
+                         uint32_t period, uint64_t i) {
     m->c[s] += inc;
     m->total += inc;
-    if (m->total > limit)
-        for (uint32_t i = 0; i < m->n; ++i) m->c[i] = (m->c[i] + 1) >> 1;
+    if ((i + 1) % period == 0 && m->total > limit)
+        for (uint32_t j = 0; j < m->n; ++j) m->c[j] = (m->c[j] + 1) >> 1;
     m->cum[0] = 0;
     for (uint32_t i = 0; i < m->n; ++i) m->cum[i + 1] = m->cum[i] + m->c[i];
     m->total = m->cum[m->n];
 }
 
-uint32_t orc_encode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit,
+uint32_t orc_encode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit, uint32_t period,
                              const uint8_t* syms, uint64_t n, uint8_t* out, uint64_t cap,
                              uint64_t* out_len) {
     adapt_model m;
@@ -142,7 +145,7 @@ uint32_t orc_encode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit,
         int k = orc_param_update(&rc, m.c[s], m.cum[s], m.total, tmp);
         for (int j = 0; j < k; ++j, ++len)
             if (len < cap) out[len] = tmp[j];
-        adapt_update(&m, s, inc, limit);
+        adapt_update(&m, s, inc, limit, period, i);
     }
     for (int j = 0; j < 8; ++j, ++len) {
         uint8_t b = left_shift(&rc);
@@ -152,7 +155,7 @@ uint32_t orc_encode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit,
     return len > cap ? ORC_F_CAPACITY : 0u;
 }
 
-uint32_t orc_decode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit,
+uint32_t orc_decode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit, uint32_t period,
                              const uint8_t* code, uint64_t code_len, uint64_t n, uint8_t* syms_out) {
     adapt_model m;
     orc_range_coder rc;
@@ -169,7 +172,7 @@ uint32_t orc_decode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit,
         if (pos + (uint64_t)k > code_len) return ORC_F_TRUNCATED;
         for (int j = 0; j < k; ++j) data = (data << 8) | code[pos++];
         syms_out[i] = (uint8_t)s;
-        adapt_update(&m, s, inc, limit);
+        adapt_update(&m, s, inc, limit, period, i);
     }
     return 0;
 }

@@ -60,12 +60,15 @@ void orc_decode_batch(const uint32_t* c, const uint32_t* cum, uint32_t n_alpha, 
                       uint8_t* syms_out, const uint64_t* sym_off, uint32_t n_chunks,
                       uint32_t* flags, int threads);
 
-/* Build-defined adaptive order-0 model (not in the reference):
- * c[i] = 1 initially, +inc after each coded symbol, halve (c = (c+1)>>1) when total > limit. */
-uint32_t orc_encode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit,
+/* Build-defined adaptive order-0 model (not in the reference), per chunk:
+ * c[i] = 1 for i < n_alpha; after coding the i-th symbol s (0-based): c[s] += inc, and if
+ * (i + 1) % period == 0 and the total exceeds limit, every c = (c + 1) >> 1.
+ * The coder sees (c[s], cum[s], total) of the model BEFORE the update, through the reference's
+ * PModel interface (pmodel.rs:4-12); the decoder's index search is FreqTable::find_index's. */
+uint32_t orc_encode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit, uint32_t period,
                              const uint8_t* syms, uint64_t n, uint8_t* out, uint64_t cap,
                              uint64_t* out_len);
-uint32_t orc_decode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit,
+uint32_t orc_decode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit, uint32_t period,
                              const uint8_t* code, uint64_t code_len, uint64_t n, uint8_t* syms_out);
 
 /* FNV-1a 64 of a byte string (used by the known-answer tests). */

@@ -190,3 +190,42 @@ def encode_stream(table, symbols):
 def decode_stream(table, code, n):
     dec = Decoder(code)
     return [dec.decode(table) for _ in range(n)]
+
+
+class AdaptiveModel(FreqTable):
+    """The build-defined adaptive order-0 model (not in the reference), as a
+    PModel on top of FreqTable: c[i] = 1 initially; after the i-th coded symbol s (0-based),
+    c[s] += inc and, every period-th symbol, halve all counts (rounding up) if the total
+    exceeds limit.  Same rule as orc_encode_adaptive / orc_decode_adaptive in rc_oracle.c."""
+
+    def __init__(self, alphabet_count, inc, limit, period):
+        super().__init__(alphabet_count)
+        self.inc, self.limit, self.period = inc, limit, period
+        self.c = [1] * alphabet_count
+        self.calc_cum()
+
+    def update(self, s, i):
+        self.c[s] += self.inc
+        if (i + 1) % self.period == 0 and sum(self.c) > self.limit:
+            self.c = [(x + 1) >> 1 for x in self.c]
+        self.calc_cum()
+
+
+def encode_adaptive_stream(n_alpha, inc, limit, period, symbols):
+    m = AdaptiveModel(n_alpha, inc, limit, period)
+    enc = Encoder()
+    for i, s in enumerate(symbols):
+        enc.encode(m, s)
+        m.update(s, i)
+    return bytes(enc.finish())
+
+
+def decode_adaptive_stream(n_alpha, inc, limit, period, code, n):
+    m = AdaptiveModel(n_alpha, inc, limit, period)
+    dec = Decoder(code)
+    out = []
+    for i in range(n):
+        s = dec.decode(m)
+        m.update(s, i)
+        out.append(s)
+    return out

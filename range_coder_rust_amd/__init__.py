@@ -1,7 +1,7 @@
 """range_coder_rust_amd — MI355X-native batched range coder (drop-in for the encode/decode path
 of diegodox/range_coder_rust).  See DESIGN.md and include/range_coder.h."""
 from .api import (  # noqa: F401
-    BadSymbolError, CapacityError, Context, CorruptStreamError, Decoder, Encoder, FreqTable,
+    ADAPTIVE_DEFAULTS, AdaptiveModel, BadSymbolError, CapacityError, Context, CorruptStreamError, Decoder, Encoder, FreqTable,
     PModel, RangeCoderError, StaticModel, TruncatedStreamError, ZeroFrequencyError,
     decode_batch, decode_chunks, default_context, encode_batch, encode_chunks, flag_names,
     slot_capacity,

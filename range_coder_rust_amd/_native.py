@@ -26,8 +26,8 @@ F_CORRUPT = 16
 EXPORTS = (
     "rc_ctx_create", "rc_ctx_destroy", "rc_ctx_set_stream", "rc_ctx_reset_stream",
     "rc_ctx_synchronize",
-    "rc_status_string", "rc_last_error", "rc_device_info", "rc_model_create_static", "rc_model_create_adaptive",
-    "rc_model_destroy", "rc_encode_batch", "rc_decode_batch", "rc_encode_host",
+    "rc_status_string", "rc_last_error", "rc_device_info", "rc_model_create_static",
+    "rc_model_create_adaptive", "rc_model_destroy", "rc_encode_batch", "rc_decode_batch", "rc_encode_host",
     "rc_decode_host", "rc_synth_fill",
 )
 
@@ -67,7 +67,7 @@ def load():
     L.rc_last_error.restype = ctypes.c_char_p
     L.rc_device_info.argtypes = [_I, ctypes.c_char_p, ctypes.c_size_t]
     L.rc_model_create_static.argtypes = [_P, _U32, _P, _P, _U32, ctypes.POINTER(_P)]
-    L.rc_model_create_adaptive.argtypes = [_P, _U32, _U32, _U32, ctypes.POINTER(_P)]
+    L.rc_model_create_adaptive.argtypes = [_P, _U32, _U32, _U32, _U32, ctypes.POINTER(_P)]
     L.rc_model_destroy.argtypes = [_P]
     L.rc_encode_batch.argtypes = [_P, _P, _P, _P, _U32, _P, _P, _P, _P]
     L.rc_decode_batch.argtypes = [_P, _P, _P, _P, _P, _P, _P, _U32, _P]

@@ -277,6 +277,39 @@ class StaticModel:
             pass
 
 
+# config C4's adaptive model parameters (include/range_coder.h, rc_model_create_adaptive)
+ADAPTIVE_DEFAULTS = dict(increment=32, limit=57343, period=256)
+
+
+class AdaptiveModel:
+    """rc_model of the build-defined adaptive order-0 model: per chunk,
+    c[i] = 1 initially; after the i-th coded symbol s, c[s] += increment and, every period-th
+    symbol, all counts are halved (rounding up) if the total exceeds limit.  Each chunk starts
+    from the initial counts, on the GPU as in the oracle (orc_encode_adaptive)."""
+
+    def __init__(self, n_symbols=256, increment=32, limit=57343, period=256, ctx=None):
+        self.ctx = ctx or default_context()
+        self.n_symbols, self.increment = int(n_symbols), int(increment)
+        self.limit, self.period = int(limit), int(period)
+        h = ctypes.c_void_p()
+        rc = self.ctx._lib.rc_model_create_adaptive(self.ctx.handle, self.n_symbols,
+                                                    self.increment, self.limit, self.period,
+                                                    ctypes.byref(h))
+        if rc == N.RC_E_BAD_MODEL:
+            raise ValueError("adaptive model rejected: need 1..256 symbols, increment >= 1, "
+                             "period a power of two, n + increment*period <= limit <= "
+                             "65535 - increment*period")
+        N.check(rc, "rc_model_create_adaptive")
+        self.handle = h
+
+    def max_bits_per_symbol(self):
+        # the rarest symbol has c >= 1 of a total < 2^16
+        return 16.0
+
+    close = StaticModel.close
+    __del__ = StaticModel.__del__
+
+
 # ----------------------------------------------------------------------------- batch API
 def slot_capacity(n_symbols, bits_per_symbol, slack=1.02):
     """A per-chunk output slot size (16-B multiple) for n symbols at a given worst bit cost."""

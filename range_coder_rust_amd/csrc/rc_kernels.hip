@@ -19,16 +19,8 @@
 //    ring and are written by cooperative flush rounds, 16 chunks x 64 B per store instruction;
 //  * decoder: the code is read 64 B per lane into a per-lane LDS ring one 16-symbol phase
 //    ahead; decoded symbols are written 16 B per lane per phase.
-#include <hip/hip_runtime.h>
+#include "rc_common.h"
 
-#include <stdint.h>
-
-#include "../../include/range_coder.h"
-
-typedef uint64_t u64;
-typedef uint32_t u32;
-
-#define TOP16 (1ull << 48)
 #define WG 256
 #define WAVES (WG / 64)
 #define ENC_RING 32          // dwords per lane in the encoder's output ring (128 B)
@@ -38,15 +30,6 @@ typedef uint32_t u32;
 #define LUT_MAX_ENTRIES (1u << LUT_BITS)
 
 enum { DIV_POW2 = 0, DIV_MAGIC = 1 };
-
-// VGPR allocation floor.  On this gfx950 stack a kernel allocated 88 VGPRs (an odd number of
-// 8-register granules) corrupts co-resident waves on the same SIMD, while the identical
-// instruction stream allocated 96 VGPRs is correct.  Each kernel clobbers a
-// register so its allocation is a multiple of 16; build() rejects any other count.
-#define RC_VGPR_FLOOR_96() asm volatile("; vgpr floor 96" ::: "v95")
-#define RC_VGPR_FLOOR_64() asm volatile("; vgpr floor 64" ::: "v63")
-#define RC_VGPR_FLOOR_112() asm volatile("; vgpr floor 112" ::: "v111")
-#define RC_VGPR_FLOOR_128() asm volatile("; vgpr floor 128" ::: "v127")
 
 struct ModelArgs {
   const uint2* tab;  // [256] (cum, c); entries s >= n_symbols hold (0xFFFFFFFF, 0)
@@ -62,8 +45,6 @@ struct ModelArgs {
 };
 
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-
-static __device__ __forceinline__ u32 hi32(u64 v) { return (u32)(v >> 32); }
 
 // RangeCoder::range_par_total (range_coder.rs:38-40): range / total, exact.
 template <int DIV>
@@ -689,7 +670,7 @@ struct rc_model {
   int div;
   ModelArgs args;
   void* dmem;
-  u32 inc, limit;  // adaptive parameters
+  AdaptParams ap;  // kind 1
 };
 
 namespace {
@@ -885,19 +866,26 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
   mm->div = pow2 ? DIV_POW2 : DIV_MAGIC;
   mm->args = a;
   mm->dmem = d;
-  mm->inc = mm->limit = 0;
+  mm->ap = AdaptParams{};
   *out = mm;
   return RC_OK;
 }
 
 rc_status rc_model_create_adaptive(rc_ctx* ctx, uint32_t n_symbols, uint32_t increment,
-                                   uint32_t limit, rc_model** out) {
-  (void)ctx;
-  (void)n_symbols;
-  (void)increment;
-  (void)limit;
-  if (out) *out = nullptr;
-  return RC_E_ARG;  // implemented in rc_adaptive (next milestone)
+                                   uint32_t limit, uint32_t period, rc_model** out) {
+  if (!ctx || !out) return RC_E_ARG;
+  *out = nullptr;
+  const u64 grow = (u64)increment * period;  // total growth between two halving checks
+  if (n_symbols < 1 || n_symbols > 256 || increment < 1 || period < 1 || period > 65536 ||
+      (period & (period - 1)) != 0 || grow + n_symbols > limit || limit + grow > 65535)
+    return RC_E_BAD_MODEL;
+  rc_model* mm = new rc_model;
+  memset(mm, 0, sizeof *mm);
+  mm->kind = 1;
+  mm->device = ctx->device;
+  mm->ap = AdaptParams{n_symbols, increment, limit, period - 1};
+  *out = mm;
+  return RC_OK;
 }
 
 rc_status rc_model_destroy(rc_model* m) {
@@ -914,9 +902,14 @@ rc_status rc_encode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   if (!ctx || !m || n_chunks > RC_MAX_CHUNKS) return RC_E_ARG;
   if (n_chunks == 0) return RC_OK;
   if (!syms || !sym_off || !out || !out_off || !out_len || !flags) return RC_E_ARG;
-  if (m->kind != 0 || m->device != ctx->device) return RC_E_ARG;
+  if (m->device != ctx->device) return RC_E_ARG;
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
+  if (m->kind == 1) {
+    const hipError_t e = rc_adaptive_encode_launch(ctx->cur, m->ap, syms, sym_off, n_chunks,
+                                                   out, out_off, out_len, flags);
+    return e == hipSuccess ? RC_OK : device_error(e, "adaptive encode launch");
+  }
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
   const bool sm = m->args.total >= 256 && m->args.total <= 65536;
 #define RC_ENC_LAUNCH(D, S)                                                                \
@@ -937,9 +930,14 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   if (!ctx || !m || n_chunks > RC_MAX_CHUNKS) return RC_E_ARG;
   if (n_chunks == 0) return RC_OK;
   if (!code || !code_off || !code_len || !syms_out || !sym_off || !flags) return RC_E_ARG;
-  if (m->kind != 0 || m->device != ctx->device) return RC_E_ARG;
+  if (m->device != ctx->device) return RC_E_ARG;
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
+  if (m->kind == 1) {
+    const hipError_t e = rc_adaptive_decode_launch(ctx->cur, m->ap, code, code_off, code_len,
+                                                   syms_out, sym_off, n_chunks, flags);
+    return e == hipSuccess ? RC_OK : device_error(e, "adaptive decode launch");
+  }
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
   const bool sm = m->args.total >= 256 && m->args.total <= 65536;
 #define RC_DEC_LAUNCH(D, S, L)                                                             \

@@ -80,14 +80,16 @@ def fixtures():
             res.append(dict(config=name, seed=seed, chunk=k, n=1024, c=[int(x) for x in c],
                             total=int(total), symbols_hex=bytes(syms).hex(), encoded_hex=b.hex()))
     inv = synth.inverse_cdf(cz)
-    for k in range(4):
-        syms = synth.host_chunk(seed, inv, k, 1024)
-        f, b, L = cpu.encode_adaptive(256, 32, 1 << 16, syms)
+    for k in range(4):  # 4096 symbols: long enough for the count halving to trigger
+        syms = synth.host_chunk(seed, inv, k, 4096)
+        f, b, L = cpu.encode_adaptive(256, 32, 57343, 256, syms)
         assert f == 0
-        f2, d = cpu.decode_adaptive(256, 32, 1 << 16, b, len(syms))
+        assert b == R.encode_adaptive_stream(256, 32, 57343, 256, syms.tolist())
+        f2, d = cpu.decode_adaptive(256, 32, 57343, 256, b, len(syms))
         assert f2 == 0 and bytes(d) == bytes(syms)
-        res.append(dict(config="C4_adaptive", seed=seed, chunk=k, n=1024, inc=32, limit=1 << 16,
-                        n_alpha=256, symbols_hex=bytes(syms).hex(), encoded_hex=b.hex()))
+        res.append(dict(config="C4_adaptive", seed=seed, chunk=k, n=4096, inc=32, limit=57343,
+                        period=256, n_alpha=256, symbols_hex=bytes(syms).hex(),
+                        encoded_hex=b.hex()))
     return res
 
 

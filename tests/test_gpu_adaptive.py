@@ -1,0 +1,160 @@
+"""GPU parity of the adaptive order-0 model: the HIP kernels
+(k_encode_adaptive / k_decode_adaptive through the C ABI) against the C oracle
+(orc_encode_adaptive / orc_decode_adaptive), byte for byte, with lengths and flags."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import range_coder_rust_amd as rc  # noqa: E402
+from range_coder_rust_amd import synth  # noqa: E402
+from oracle import cpu  # noqa: E402
+from gpu_helpers import dev, run_decode, run_encode  # noqa: E402
+
+C4 = (32, 57343, 256)  # increment, limit, period
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return rc.default_context(0)
+
+
+def zipf_syms(rng, n_alpha, n, s=1.2):
+    w = 1.0 / np.arange(1, n_alpha + 1) ** s
+    return rng.choice(n_alpha, size=n, p=w / w.sum()).astype(np.uint8)
+
+
+def oracle_enc(n_alpha, params, syms):
+    return cpu.encode_adaptive(n_alpha, *params, syms)
+
+
+def test_c4_fixtures_gpu(ctx, golden_dir):
+    with open(os.path.join(golden_dir, "fixtures.json")) as f:
+        fx = [e for e in json.load(f) if e["config"] == "C4_adaptive"]
+    assert fx
+    e0 = fx[0]
+    m = rc.AdaptiveModel(e0["n_alpha"], e0["inc"], e0["limit"], e0["period"], ctx=ctx)
+    chunks = [np.frombuffer(bytes.fromhex(e["symbols_hex"]), np.uint8) for e in fx]
+    caps = [rc.slot_capacity(len(c), 16) for c in chunks]
+    out, out_off, ol, fl = run_encode(m, chunks, caps)
+    for k, e in enumerate(fx):
+        want = bytes.fromhex(e["encoded_hex"])
+        assert fl[k] == 0 and ol[k] == len(want)
+        assert bytes(out[out_off[k]:out_off[k] + ol[k]]) == want
+    dec, fd = run_decode(m, [bytes.fromhex(e["encoded_hex"]) for e in fx],
+                         [len(c) for c in chunks])
+    assert (fd == 0).all()
+    for k in range(len(fx)):
+        assert bytes(dec[k]) == bytes(chunks[k])
+
+
+PARAMS = [(256, *C4), (2, 1, 300, 1), (17, 5, 1000, 4), (1, 7, 600, 8), (256, 255, 8160, 16),
+          (40, 32, 8192, 64), (256, 1, 300, 1)]
+
+
+@pytest.mark.parametrize("params", PARAMS)
+@pytest.mark.parametrize("misalign", [False, True])
+def test_random_chunks_vs_oracle(ctx, params, misalign):
+    n_alpha, inc, limit, period = params
+    rng = np.random.default_rng(n_alpha * 1000 + inc + misalign)
+    lens = [0, 1, 2, 3, 5, 8, 63, 64, 65, 257, 1000, 4096, 5003] + \
+        list(rng.integers(0, 3000, 51))  # 64 chunks: one full wave, ragged
+    chunks = [zipf_syms(rng, n_alpha, int(L), s=float(rng.uniform(0.0, 1.6))) for L in lens]
+    m = rc.AdaptiveModel(n_alpha, inc, limit, period, ctx=ctx)
+    caps = [rc.slot_capacity(len(c), 16) for c in chunks]
+    out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=misalign, seed=inc)
+    codes = []
+    for k, c in enumerate(chunks):
+        f, want, L = oracle_enc(n_alpha, (inc, limit, period), c)
+        assert fl[k] == f == 0 and ol[k] == L, k
+        got = bytes(out[out_off[k]:out_off[k] + ol[k]])
+        assert got == want, f"chunk {k} (len {len(c)})"
+        codes.append(want)
+    dec, fd = run_decode(m, codes, [len(c) for c in chunks], misalign=misalign, seed=inc)
+    assert (fd == 0).all()
+    for k, c in enumerate(chunks):
+        assert bytes(dec[k]) == bytes(c), k
+
+
+def test_adaptive_error_flags(ctx):
+    n_alpha, inc, limit, period = 10, 32, 8448, 256
+    m = rc.AdaptiveModel(n_alpha, inc, limit, period, ctx=ctx)
+    rng = np.random.default_rng(3)
+    good = zipf_syms(rng, n_alpha, 3000)
+    bad = good.copy()
+    bad[1234] = 10  # outside the alphabet
+    chunks = [good, bad, np.zeros(0, np.uint8), good[:100]]
+    f, full, L = oracle_enc(n_alpha, (inc, limit, period), good)
+    caps = [rc.slot_capacity(3000, 16), rc.slot_capacity(3000, 16), 64, 16]
+    out, out_off, ol, fl = run_encode(m, chunks, caps)
+    fb, _, Lb = oracle_enc(n_alpha, (inc, limit, period), bad)
+    fs, short, Ls = oracle_enc(n_alpha, (inc, limit, period), good[:100])
+    assert list(fl) == [0, rc.api.N.F_BAD_SYMBOL, 0, rc.api.N.F_CAPACITY]
+    assert fb == rc.api.N.F_BAD_SYMBOL and ol[1] == Lb
+    assert ol[3] == Ls and bytes(out[out_off[3]:out_off[3] + 16]) == short[:16]
+    assert ol[2] == 8 and bytes(out[out_off[2]:out_off[2] + 8]) == bytes(8)
+    # decoder: truncated streams and codes shorter than 8 bytes
+    codes = [full, full[:-1], full[:len(full) // 2], full[:7], full[:8]]
+    counts = [3000, 3000, 3000, 1, 0]
+    dec, fd = run_decode(m, codes, counts)
+    for k in range(len(codes)):
+        f, d = cpu.decode_adaptive(n_alpha, inc, limit, period, codes[k], counts[k])
+        assert fd[k] == f, k
+    assert list(fd) == [0, 8, 8, 8, 0]
+    # garbage streams decode like the oracle (no detection, as in the reference)
+    garbage = [bytes(rng.integers(0, 256, 600).astype(np.uint8)) for _ in range(8)]
+    dec, fd = run_decode(m, garbage, [500] * 8)
+    for k, g in enumerate(garbage):
+        f, d = cpu.decode_adaptive(n_alpha, inc, limit, period, g, 500)
+        assert fd[k] == f
+        if f == 0:
+            assert bytes(dec[k]) == bytes(d)
+
+
+def test_adaptive_model_validation(ctx):
+    ok = [(256, *C4), (1, 1, 2, 1), (256, 1, 65534 - 1, 1)]
+    bad = [(0, *C4), (257, *C4), (256, 0, 57343, 256), (256, 32, 57343, 3),
+           (256, 32, 57344, 256), (256, 32, 8447, 256), (256, 32, 57343, 1 << 17)]
+    for n, i, l, p in ok:
+        rc.AdaptiveModel(n, i, l, p, ctx=ctx).close()
+    for n, i, l, p in bad:
+        with pytest.raises(ValueError):
+            rc.AdaptiveModel(n, i, l, p, ctx=ctx)
+
+
+def test_c4_scale_round_trip(ctx):
+    """C4 at 2^16 x 16 KiB chunks (1 GiB): round trip + a seeded sample against the oracle."""
+    n, L = 1 << 16, 16384
+    c, _, _ = synth.zipf_table()
+    inv = synth.inverse_cdf(c)
+    seed = 0x5EED0004
+    syms = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    synth.fill(ctx, seed, inv, syms, L, n)
+    m = rc.AdaptiveModel(256, *C4, ctx=ctx)
+    cap = rc.slot_capacity(L, 16)
+    so = torch.arange(n + 1, dtype=torch.int64, device="cuda") * L
+    oo = torch.arange(n + 1, dtype=torch.int64, device="cuda") * cap
+    out = torch.empty(n * cap, dtype=torch.uint8, device="cuda")
+    ol, fl = rc.encode_batch(m, syms, so, out, oo)
+    dec = torch.empty_like(syms)
+    fd = rc.decode_batch(m, out, oo[:-1].contiguous(), ol, dec, so)
+    torch.cuda.synchronize()
+    assert int(fl.abs().sum()) == 0 and int(fd.abs().sum()) == 0
+    assert torch.equal(dec, syms)
+    bps = float(ol.sum()) / (n * L)
+    assert 0.6 < bps < 0.75, bps  # Zipf(1.2) entropy ~0.661 B/sym plus adaptation cost
+    olh = ol.cpu().numpy()
+    rng = np.random.default_rng(5)
+    for k in [0, n - 1] + list(rng.integers(0, n, 6)):
+        k = int(k)
+        host = synth.host_chunk(seed, inv, k, L)
+        f, want, Lk = oracle_enc(256, C4, host)
+        assert f == 0 and olh[k] == Lk
+        assert bytes(out[k * cap: k * cap + Lk].cpu().numpy()) == want

@@ -54,7 +54,7 @@ def test_fixtures(golden_dir):
     for e in fx:
         syms = bytes.fromhex(e["symbols_hex"])
         if e["config"] == "C4_adaptive":
-            f, b, _ = cpu.encode_adaptive(e["n_alpha"], e["inc"], e["limit"], syms)
+            f, b, _ = cpu.encode_adaptive(e["n_alpha"], e["inc"], e["limit"], e["period"], syms)
         else:
             f, b, _ = cpu.encode(e["c"], cum_of(e["c"]), e["total"], syms)
         assert f == 0 and b.hex() == e["encoded_hex"]
@@ -136,7 +136,28 @@ def test_batch_threads_match_single():
 def test_adaptive_round_trip():
     rng = np.random.default_rng(7)
     syms = rng.integers(0, 40, 5000).astype(np.uint8)
-    f, b, L = cpu.encode_adaptive(40, 32, 1 << 16, syms)
+    f, b, L = cpu.encode_adaptive(40, 32, 57343, 256, syms)
     assert f == 0
-    f, d = cpu.decode_adaptive(40, 32, 1 << 16, b, len(syms))
+    f, d = cpu.decode_adaptive(40, 32, 57343, 256, b, len(syms))
     assert f == 0 and (d == syms).all()
+
+
+@pytest.mark.parametrize("n_alpha,inc,limit,period,n", [
+    (256, 32, 57343, 256, 3000), (2, 1, 300, 1, 2000), (17, 5, 1000, 4, 2500),
+    (1, 7, 600, 8, 300), (256, 255, 255 * 16, 16, 1500)])
+def test_adaptive_oracle_matches_literal_restatement(n_alpha, inc, limit, period, n):
+    """The C adaptive model against oracle/ref_literal.py's PModel-based restatement."""
+    rng = np.random.default_rng(n_alpha * 7 + inc)
+    w = 1.0 / np.arange(1, n_alpha + 1) ** 1.1
+    syms = rng.choice(n_alpha, size=n, p=w / w.sum()).astype(np.uint8)
+    f, b, L = cpu.encode_adaptive(n_alpha, inc, limit, period, syms)
+    assert f == 0 and L == len(b)
+    assert b == R.encode_adaptive_stream(n_alpha, inc, limit, period, syms.tolist())
+    f, d = cpu.decode_adaptive(n_alpha, inc, limit, period, b, n)
+    assert f == 0 and (d == syms).all()
+    assert R.decode_adaptive_stream(n_alpha, inc, limit, period, b, n) == syms.tolist()
+    # a truncated stream is flagged where the literal restatement panics
+    f, _ = cpu.decode_adaptive(n_alpha, inc, limit, period, b[:-1], n)
+    with pytest.raises(R.ReferencePanic):
+        R.decode_adaptive_stream(n_alpha, inc, limit, period, b[:-1], n)
+    assert f == 8  # RC_F_TRUNCATED
