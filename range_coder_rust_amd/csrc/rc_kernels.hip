@@ -44,7 +44,6 @@ struct ModelArgs {
   u32 direct;        // 1: lut[q] = s | cum << 8 | c << 20 for every q < total (total <= 2048)
 };
 
-typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
 // RangeCoder::range_par_total (range_coder.rs:38-40): range / total, exact.
 template <int DIV>
