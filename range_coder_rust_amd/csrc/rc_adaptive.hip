@@ -27,18 +27,6 @@
 #define AWG 64                  // one wave per workgroup
 #define TREE_BYTES (255 * 64 * 2)
 
-// a global (not flat) dword load: flat loads also count in lgkmcnt, so every LDS wait of the
-// tree walk would wait for them too
-static __device__ __forceinline__ u32 gload(const u32* p) {
-  return *(const __attribute__((address_space(1))) u32*)p;
-}
-static __device__ __forceinline__ void gstore8(uint8_t* p, u32 v) {
-  *(__attribute__((address_space(1))) uint8_t*)p = (uint8_t)v;
-}
-static __device__ __forceinline__ void gstore32(uint8_t* p, u32 v) {
-  *(__attribute__((address_space(1))) u32*)p = v;
-}
-
 // ~1/t to well under 2^-40 relative error: v_rcp_f64 plus one Newton step
 static __device__ __forceinline__ double recip(u32 t) {
   const double d = (double)t;
@@ -151,9 +139,6 @@ static __device__ void tree_halve(uint16_t* t, u32& total) {
 
 __device__ u32x4 g_zero16;  // load target of lanes without input (never written)
 
-static __device__ __forceinline__ u32x4 gload16(const u32x4* p) {
-  return *(const __attribute__((address_space(1))) u32x4*)p;
-}
 
 // 4 bytes at byte offset (dsh * 4 + bsh) of the 8-dword window v: v[dsh], v[dsh + 1] funnel
 static __device__ __forceinline__ u32 pick4(const u32 (&v)[8], u32 k, u32 dsh, u32 bsh) {

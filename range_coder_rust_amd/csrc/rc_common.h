@@ -23,6 +23,20 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
 static __device__ __forceinline__ u32 hi32(u64 v) { return (u32)(v >> 32); }
 
+// Global (not flat) memory access.  A flat access also counts in lgkmcnt, so every LDS wait
+// would wait for it too; pointers that pass through LDS or integer casts lose their address
+// space and compile to flat unless cast back like this.
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) u32 g_u32;
+typedef __attribute__((address_space(1))) u64 g_u64;
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+static __device__ __forceinline__ u32 gload(const u32* p) { return *(const g_u32*)p; }
+static __device__ __forceinline__ u32x4 gload16(const u32x4* p) { return *(const g_u32x4*)p; }
+static __device__ __forceinline__ void gstore8(uint8_t* p, u32 v) { *(g_u8*)p = (uint8_t)v; }
+static __device__ __forceinline__ void gstore32(uint8_t* p, u32 v) { *(g_u32*)p = v; }
+static __device__ __forceinline__ void gstore64(uint8_t* p, u64 v) { *(g_u64*)p = v; }
+static __device__ __forceinline__ void gstore128(uint8_t* p, u32x4 v) { *(g_u32x4*)p = v; }
+
 // Adaptive order-0 model parameters (rc_model_create_adaptive)
 struct AdaptParams {
   u32 n;      // alphabet size (1..256)

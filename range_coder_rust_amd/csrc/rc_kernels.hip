@@ -114,13 +114,18 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
       const EncOut o = wout[c];
       const u32 p0 = fp + 16 * g;
       if (p0 >= o.lo_ok && p0 + 16 <= o.hi_ok) {
-        *reinterpret_cast<uint4*>(o.gbase + p0) = v;
+        u32x4 g16;
+        g16.x = v.x;
+        g16.y = v.y;
+        g16.z = v.z;
+        g16.w = v.w;
+        gstore128(o.gbase + p0, g16);
       } else {
         const u32 w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const u32 p = p0 + j;
-          if (p >= o.lo_ok && p < o.hi_ok) o.gbase[p] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+          if (p >= o.lo_ok && p < o.hi_ok) gstore8(o.gbase + p, w[j >> 2] >> (8 * (j & 3)));
         }
       }
     }
