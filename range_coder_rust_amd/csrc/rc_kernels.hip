@@ -362,7 +362,8 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
 // ring covers (rare renormalisation bursts) are refilled synchronously.
 // ------------------------------------------------------------------------------------------
 struct Dec {
-  u64 low, range, data;  // RangeCoder + Decoder::data (decoder.rs:6-12)
+  u64 low, range;  // RangeCoder (decoder.rs:6-12)
+  u64 x;           // Decoder::data - lower_bound (mod 2^64): all find_index needs (sample_impl.rs:29)
   u32 cpos;   // bytes consumed, relative to the 16-B aligned base of the code stream
   u32 fill;   // bytes staged into the ring, same origin
   u32 lim;    // cpos > lim: more bytes consumed than the stream holds
@@ -412,31 +413,38 @@ static __device__ __forceinline__ void dec_phase(Dec& d) {
 }
 
 // a lane about to read past the staged bytes: commit / load synchronously (rare)
-static __device__ __forceinline__ void dec_sync(Dec& d) {
-  while ((int)(d.fill - d.cpos) < 4) {
+static __device__ __forceinline__ void dec_sync(Dec& d, u32 need) {
+  while ((int)(d.fill - d.cpos) < (int)need) {
     if (!d.pend_ok) dec_issue(d);
     dec_commit(d);
   }
 }
 
-// data = the 8 code bytes ending at cpos, big-endian (Decoder::shift_left_buffer, :31-35)
-static __device__ __forceinline__ void dec_window(Dec& d) {
+// the 8 code bytes ending at cpos, big-endian (Decoder::new's priming, decoder.rs:14-23)
+static __device__ __forceinline__ u64 dec_read8_before(const Dec& d) {
   const u32 p = d.cpos - 8;
   const u32* rp = d.ring + ((p >> 2) & (DEC_RING - 1)) * 64;
   const u32 d0 = rp[0], d1 = rp[64], d2 = rp[128];
   const u32 sh = p & 3;
   const u32 w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
   const u32 w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-  d.data = ((u64)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
+  return ((u64)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
 }
 
-static __device__ __forceinline__ void dec_rare(Dec& d) {
-  // range_reduction_expansion (range_coder.rs:126-135); the decoder only counts the bytes
+// range_reduction_expansion (range_coder.rs:126-135): each iteration settles one more byte,
+// which Decoder::shift_left_buffer (decoder.rs:31-35) shifts into data (so into x = data-low)
+static __device__ __forceinline__ void dec_rare(Dec& d, u32 need) {
+  u32 m = 0;
   while (d.range < TOP16) {
     d.range = ~d.low & (TOP16 - 1);
     d.low <<= 8;
     d.range <<= 8;
-    d.cpos += 1;
+    ++m;
+  }
+  dec_sync(d, m + need);
+  for (u32 j = 0; j < m; ++j, ++d.cpos) {
+    const u32 w = d.ring[((d.cpos >> 2) & (DEC_RING - 1)) * 64];
+    d.x = (d.x << 8) | ((w >> (8 * (d.cpos & 3))) & 255u);
   }
 }
 
@@ -473,13 +481,12 @@ static __device__ __forceinline__ float cvt_f32(u32 v) {
 template <int DIV, int SM, int LUT>
 static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const uint2* s_tab,
                                               const u32* s_lut) {
-  // speculative read of the next window: bytes [cpos - 8, cpos - 8 + 16 (+4)) cover any
-  // common-path consumption (<= 3 bytes, <= 7 when !SM)
-  const u32 p0 = d.cpos - 8;
-  const u32* rp = d.ring + ((p0 >> 2) & (DEC_RING - 1)) * 64;
-  const u32 D0 = rp[0], D1 = rp[64], D2 = rp[128], D3 = rp[192];
-  const u32 D4 = SM ? 0u : rp[256];
-  const u64 x = d.data - d.low;
+  // the code bytes at cpos (the ring holds >= 4 of them, >= 8 when !SM): the ones this
+  // symbol settles are shifted into x at the end
+  const u32* rp = d.ring + ((d.cpos >> 2) & (DEC_RING - 1)) * 64;
+  const u32 D0 = rp[0], D1 = rp[64];
+  const u32 D2 = SM ? 0u : rp[128];
+  const u64 x = d.x;
   const u64 r = range_par_total<DIV>(d.range, m);
   // hint q ~ x / r ~ x * total / range from the top 32 bits of x and range, both shifted by
   // clz(range) (range >= 2^48, so the shift is < 16); relative error ~2^-22
@@ -517,25 +524,25 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   const u32 k8 = SM ? ((u32)__builtin_clz(hi32(xx)) & 24u) : ((u32)__clzll(xx) & 56u);
   d.low <<= k8;
   d.range <<= k8;
-  const u32 kb = k8 >> 3;
-  d.cpos += kb;
-  // next window from the speculative read
-  const u32 o = (p0 & 3) + kb;  // byte offset of the new window in D0..D4
-  const u32 i = o >> 2, sh = o & 3;
-  const u32 Da = SM ? (i ? D1 : D0) : (i == 0 ? D0 : i == 1 ? D1 : D2);
-  const u32 Db = SM ? (i ? D2 : D1) : (i == 0 ? D1 : i == 1 ? D2 : D3);
-  const u32 Dc = SM ? (i ? D3 : D2) : (i == 0 ? D2 : i == 1 ? D3 : D4);
-  const u32 w0 = __builtin_amdgcn_alignbyte(Db, Da, sh);
-  const u32 w1 = __builtin_amdgcn_alignbyte(Dc, Db, sh);
-  d.data = ((u64)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
-  // rare: range_reduction_expansion, or the ring ran short -> re-read the window
-  const bool rare = (hi32(d.range) < 0x10000u) | ((int)(d.fill - d.cpos) < 4);
+  // data' = data << k8 | k settled bytes, low' = (low + A) << k8, so
+  // x' = ((x - A) << k8) | those bytes (shift_left_buffer, decoder.rs:31-35)
+  const u32 sh = d.cpos & 3;
+  const u32 b0 = __builtin_bswap32(__builtin_amdgcn_alignbyte(D1, D0, sh));
+  u32 nb;
+  if (SM) {  // k8 <= 24
+    nb = hi32((u64)b0 << k8);
+  } else {   // k8 <= 56
+    const u64 b = ((u64)b0 << 32) | __builtin_bswap32(__builtin_amdgcn_alignbyte(D2, D1, sh));
+    nb = 0;
+    d.x = k8 ? b >> (64 - k8) : 0ull;
+  }
+  d.x = SM ? (((x - A) << k8) | nb) : (((x - A) << k8) | d.x);
+  d.cpos += k8 >> 3;
+  // rare: range_reduction_expansion, or the ring runs short for the next symbol
+  const u32 need = SM ? 4u : 8u;
+  const bool rare = (hi32(d.range) < 0x10000u) | ((int)(d.fill - d.cpos) < (int)need);
   if (__builtin_expect(__any((int)rare), 0)) {
-    if (rare) {
-      dec_rare(d);
-      if ((int)(d.fill - d.cpos) < 4) dec_sync(d);
-      dec_window(d);
-    }
+    if (rare) dec_rare(d, need);
   }
   return s;
 }
@@ -583,7 +590,7 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   dec_issue(d);
   dec_commit(d);
   dec_issue(d);
-  dec_window(d);
+  d.x = dec_read8_before(d);  // data - low with low = 0
 
   u64 i = 0;
   u64 head = (16 - ((uintptr_t)op & 15)) & 15;
