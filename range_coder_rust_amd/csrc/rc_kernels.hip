@@ -173,10 +173,18 @@ template <int DIV, int SM>
 static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, const uint2* s_tab,
                                                 u32 sym) {
   const uint2 t = s_tab[sym];
-  const bool bad = t.y == 0;  // zero frequency (reference: endless loop) or outside alphabet
-  const u32 code = t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ;
-  e.err = (bad && e.err == 0) ? code : e.err;
-  const u32 c = bad ? 1u : t.y, cum = bad ? 0u : t.x;
+  u32 c, cum;
+  if (SM) {  // bad entries were staged as (flag << 24, 1): accumulate, sort out at the end
+    e.err |= t.x;
+    cum = t.x & 0xFFFFFFu;
+    c = t.y;
+  } else {
+    const bool bad = t.y == 0;  // zero frequency (reference: endless loop) or outside alphabet
+    const u32 code = t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ;
+    e.err = (bad && e.err == 0) ? code : e.err;
+    c = bad ? 1u : t.y;
+    cum = bad ? 0u : t.x;
+  }
   const u64 r = range_par_total<DIV>(e.range, m);
   e.range = mul_rv<SM>(r, c);   // range_coder.rs:65
   e.low += mul_rv<SM>(r, cum);  // range_coder.rs:68-81 (overflow unreachable)
@@ -243,6 +251,16 @@ static __device__ __forceinline__ void enc_byte_sym(Enc& e, const ModelArgs& m,
   enc_sym<DIV, SM>(e, m, s_tab, sym, act, lane, wring, wout);
 }
 
+// the first symbol of a chunk the reference cannot encode (rare: flagged chunks only)
+static __device__ u32 enc_first_error(const ModelArgs& m, const uint8_t* sp, u64 n) {
+  for (u64 i = 0; i < n; ++i) {
+    const u32 s = sp[i];
+    if (s >= m.n) return RC_F_BAD_SYMBOL;  // sample_impl.rs:19 (Vec::get().unwrap())
+    if (m.tab[s].y == 0) return RC_F_ZERO_FREQ;  // range_coder.rs:83-85 (endless loop)
+  }
+  return 0;
+}
+
 template <int DIV, int SM>
 __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint8_t* __restrict__ syms,
                                                         const u64* __restrict__ sym_off,
@@ -254,7 +272,15 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   __shared__ u32 s_ring[WAVES * ENC_RING * 64];
   __shared__ EncOut s_out[WG];
   const u32 tid = threadIdx.x;
-  s_tab[tid] = m.tab[tid];
+  {
+    // SM (cum < 2^16): a symbol the reference cannot encode (c == 0: endless loop; outside the
+    // alphabet: panic) is staged as (flag << 24, c = 1), so the common path only ORs entries
+    // together; a chunk whose OR shows a flag is re-scanned for its first error at the end
+    uint2 t = m.tab[tid];
+    if (SM && t.y == 0)
+      t = make_uint2((t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ) << 24, 1u);
+    s_tab[tid] = t;
+  }
   const u32 lane = tid & 63, wave = tid >> 6;
   const u32 k = blockIdx.x * WG + tid;
   const bool live = k < n_chunks;  // dead lanes still take part in the wave's flush rounds
@@ -345,6 +371,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   if (end < s_out[tid].hi_ok) s_out[tid].hi_ok = end;
   while (__any((int)(e.fpos < e.wpos))) enc_round(e, e.fpos < e.wpos, lane, wring, wout);
   if (live) {
+    if (SM) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
     if (!e.err && (u64)len > cap) e.err = RC_F_CAPACITY;
     out_len[k] = len;
     flags[k] = e.err;
@@ -508,14 +535,19 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   }
   u64 A = mul_rv<SM>(r, t.x);
   u64 B = mul_rv<SM>(r, t.y);
-  // exact verification r*cum[s] <= x < r*cum[s+1]; the hint is rarely off
-  const bool off = (A > x) | ((s + 1 < m.n) & (x - A >= B));
+  // exact verification r*cum[s] <= x < r*cum[s+1]; the hint is rarely off.  (At s = n - 1 the
+  // upper test fails only on corrupt input, x >= r * total: dec_fix keeps s = n - 1 there.)
+  const bool off = (A > x) | (x - A >= B);
   if (__builtin_expect(__any((int)off), 0)) {
-    if (off) dec_fix(s, t, A, B, x, r, s_tab, m.n);
-  }
-  if (t.y == 0) {  // only on corrupt input (reference: endless loop); an over-read came first
-    d.err = d.err ? d.err : (d.cpos > d.lim ? RC_F_TRUNCATED : RC_F_CORRUPT);
-    B = r;
+    if (off) {
+      dec_fix(s, t, A, B, x, r, s_tab, m.n);
+      // the tables only hold symbols with c > 0, so c == 0 can only come from dec_fix: corrupt
+      // input (the reference loops forever); an over-read, if any, came first
+      if (t.y == 0) {
+        d.err = d.err ? d.err : (d.cpos > d.lim ? RC_F_TRUNCATED : RC_F_CORRUPT);
+        B = r;
+      }
+    }
   }
   // param_update (range_coder.rs:53-92)
   d.low += A;

@@ -170,6 +170,39 @@ def test_error_flags_gpu(ctx):
         rc.StaticModel([1, 2], [0, 2], 3)  # cum[1] != cum[0] + c[0]
 
 
+def test_error_flags_sm_gpu(ctx):
+    """256 <= total <= 2^16 (the SM kernels): zero-frequency and out-of-alphabet symbols, both
+    orders in one chunk (the first error wins), flagged chunks among clean ones."""
+    rng = np.random.default_rng(11)
+    c = rng.integers(1, 400, 200).astype(np.uint32)
+    c[[5, 77, 150]] = 0
+    total = int(c.sum())
+    assert 256 <= total <= 65536
+    m = rc.StaticModel(c, cum_of(c), total)
+    good = [i for i in range(200) if c[i]]
+    chunks = []
+    for k in range(64):
+        ch = rng.choice(good, size=int(rng.integers(50, 3000))).astype(np.uint8)
+        kind = k % 8
+        if kind == 1:
+            ch[len(ch) // 2] = 77            # zero frequency
+        elif kind == 2:
+            ch[len(ch) // 3] = 230           # outside the alphabet
+        elif kind == 3:
+            ch[10], ch[20] = 5, 201          # zero frequency first
+        elif kind == 4:
+            ch[10], ch[20] = 255, 150        # outside the alphabet first
+        chunks.append(ch)
+    caps = [rc.slot_capacity(len(ch), 16) for ch in chunks]
+    for mis in (False, True):
+        out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=mis, seed=3)
+        for k, ch in enumerate(chunks):
+            f, want, L = cpu.encode(c, cum_of(c), total, ch)
+            assert fl[k] == f, (k, fl[k], f)
+            if f == 0:
+                assert ol[k] == L and bytes(out[out_off[k]:out_off[k] + L]) == want
+
+
 def test_bad_models_rejected_by_abi(ctx):
     """rc_model_create_static validates the PModel snapshot itself (not only the Python layer)."""
     import ctypes
