@@ -76,17 +76,27 @@ static __device__ __forceinline__ u64 mul_rv(u64 r, u32 v) {
 #define ENC_UNIT 64    // bytes per flush unit
 #define FLUSH_AT 88    // ring fill forcing a flush round: 88 + 7*3 + 3 + 11 (rare tail) < 124
 #define SINK_SLOTS 65536
-__device__ uint4 g_sink[SINK_SLOTS];  // target of masked-out bytes (never read)
+__device__ uint4 g_sink[SINK_SLOTS];  // dummy symbol tiles of dead lanes (contents irrelevant)
 
 struct Enc {
   u64 low, range;  // RangeCoder state (range_coder.rs:7-12)
-  u64 acc;         // settled bytes not yet pushed (newest in the low bits)
-  u32 nbits;       // 8 * bytes held in acc, < 32 between symbols
-  u32 wpos;        // ring byte position of the next push (from the 64-B aligned slot base)
+  u64 acc;         // settled bytes, newest in the low bits; the B & 31 lowest are not pushed
+  u32 B;           // bit position of the next settled byte, from the 64-B aligned slot base:
+                   // dword B >> 5 of the stream is the incomplete one (its ring slot is free)
   u32 fpos;        // byte position of the next unit to store
-  u32 err;         // first RC_F_* error of this chunk
+  u32 err;         // first RC_F_* error of this chunk (SM: OR of staged table flags)
   u32* ring;       // this lane's ring column: dword j at ring[j * 64]
 };
+
+// byte position of the incomplete dword (everything below it has been pushed to the ring)
+static __device__ __forceinline__ u32 enc_wpos(const Enc& e) { return (e.B >> 5) << 2; }
+
+// v_ffbh_u32 as the hardware defines it: 0xFFFFFFFF for 0 (the clz builtins are undefined there)
+static __device__ __forceinline__ u32 ffbh(u32 v) {
+  u32 r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
 
 // Per-chunk output geometry shared with the other lanes of the wave (flush rounds)
 struct EncOut {
@@ -136,19 +146,16 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
 // flush rounds until no lane's ring is above the threshold (wave-uniform call sites only)
 static __device__ __forceinline__ void enc_flush(Enc& e, u32 lane, const u32* wring,
                                                  const EncOut* wout) {
-  while (__any((int)(e.wpos - e.fpos >= FLUSH_AT)))
-    enc_round(e, e.wpos - e.fpos >= ENC_UNIT, lane, wring, wout);
+  while (__any((int)(enc_wpos(e) - e.fpos >= FLUSH_AT)))
+    enc_round(e, enc_wpos(e) - e.fpos >= ENC_UNIT, lane, wring, wout);
 }
 
 // One settled byte, with a conditional push (rare paths only).
 static __device__ __forceinline__ void enc_emit_byte(Enc& e, u32 b) {
   e.acc = (e.acc << 8) | b;
-  e.nbits += 8;
-  if (e.nbits >= 32) {
-    e.nbits -= 32;
-    e.ring[((e.wpos >> 2) & (ENC_RING - 1)) * 64] = __builtin_bswap32((u32)(e.acc >> e.nbits));
-    e.wpos += 4;
-  }
+  e.B += 8;
+  if ((e.B & 31) == 0)
+    e.ring[(((e.B >> 5) - 1) & (ENC_RING - 1)) * 64] = __builtin_bswap32((u32)e.acc);
 }
 
 // Rare tail of param_update for one lane: the no-carry loop when >= 4 bytes settle
@@ -168,14 +175,16 @@ static __device__ __forceinline__ void enc_rare(Enc& e) {
 }
 
 // Encoder::encode (encoder.rs:24-37) -> RangeCoder::param_update (range_coder.rs:53-92),
-// common path without branches.  Returns true when the lane needs enc_rare().
+// common path without branches.  Returns true when the lane needs enc_rare().  Written for the
+// gfx950 VALU price list (profiles/r01/ubench_valu.txt): 64-bit ops, multiplies, compares and
+// bit-field ops cost ~3.6 cycles per wave, plain 32-bit add/logic/right-shift ~2.
 template <int DIV, int SM>
-static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, const uint2* s_tab,
-                                                u32 sym) {
-  const uint2 t = s_tab[sym];
+static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint2 t) {
   u32 c, cum;
   if (SM) {  // bad entries were staged as (flag << 24, 1): accumulate, sort out at the end
-    e.err |= t.x;
+    // (as an asm OR: left to itself the compiler defers all the ORs to the end of the loop
+    // and spills every table entry)
+    asm volatile("v_or_b32 %0, %0, %1" : "+v"(e.err) : "v"(t.x));
     cum = t.x & 0xFFFFFFu;
     c = t.y;
   } else {
@@ -186,59 +195,63 @@ static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, cons
     cum = bad ? 0u : t.x;
   }
   const u64 r = range_par_total<DIV>(e.range, m);
-  e.range = mul_rv<SM>(r, c);   // range_coder.rs:65
-  e.low += mul_rv<SM>(r, cum);  // range_coder.rs:68-81 (overflow unreachable)
+  if (SM) {  // r < 2^56, c, cum <= 2^16: low half by v_mad_u64_u32, high by v_mad_u32_u24
+    const u32 rl = (u32)r, rh = hi32(r);
+    const u64 R0 = (u64)rl * c;                   // range_coder.rs:65
+    const u64 L0 = (u64)rl * cum + e.low;         // range_coder.rs:68-81 (no overflow, §3)
+    e.range = ((u64)(hi32(R0) + __umul24(rh, c)) << 32) | (u32)R0;
+    e.low = ((u64)(hi32(L0) + __umul24(rh, cum)) << 32) | (u32)L0;
+  } else {
+    e.range = r * (u64)c;
+    e.low += r * (u64)cum;
+  }
   // no_carry_expansion in closed form: k = clz(low ^ upper) / 8 bytes settle (<= 3 here;
-  // x == 0 means >= 4 and the rare path continues after these 3)
-  const u32 x = hi32(e.low) ^ hi32(e.low + e.range);
-  const u32 nb = (u32)__builtin_clz(x | 1u) & 24u;
-  const u32 bytes = (u32)(((u64)hi32(e.low) << nb) >> 32);
+  // equal high halves (ffbh = ~0) mean >= 4 and the rare path continues after these 3)
+  const u32 lh = hi32(e.low);
+  const u32 z = ffbh(lh ^ hi32(e.low + e.range));
+  const u32 nb = z & 24u;
+  const u32 bytes = __builtin_amdgcn_ubfe(lh, 32u - nb, nb);  // the top nb bits (0 if nb == 0)
   e.acc = (e.acc << nb) | bytes;
   e.low <<= nb;
   e.range <<= nb;
-  const u32 nbits = e.nbits + nb;
-  const bool push = nbits >= 32;
-  e.nbits = push ? nbits - 32 : nbits;
-  e.ring[((e.wpos >> 2) & (ENC_RING - 1)) * 64] = __builtin_bswap32((u32)(e.acc >> e.nbits));
-  e.wpos += push ? 4u : 0u;
-  return (x == 0) | (hi32(e.range) < 0x10000u);
+  // push: the slot of the dword that was incomplete before this symbol gets the 32 bits above
+  // the (new) incomplete ones; if it is still incomplete the slot is rewritten later
+  const u32 slot = (e.B >> 5) & (ENC_RING - 1);
+  e.B += nb;
+  e.ring[slot * 64] = __builtin_bswap32((u32)(e.acc >> (e.B & 31u)));
+  return (z > 31u) | (hi32(e.range) < 0x10000u);
 }
 
-// one symbol for the lanes with `act`; the rare path (wave-uniform branch) may flush
+// one symbol (table entry t) for the lanes with `act`; the rare path (wave-uniform branch) may
+// flush
 template <int DIV, int SM>
-static __device__ __forceinline__ void enc_sym(Enc& e, const ModelArgs& m, const uint2* s_tab,
-                                               u32 sym, bool act, u32 lane, const u32* wring,
-                                               const EncOut* wout) {
+static __device__ __forceinline__ void enc_sym(Enc& e, const ModelArgs& m, uint2 t, bool act,
+                                               u32 lane, const u32* wring, const EncOut* wout) {
   bool rare = false;
-  if (act) rare = enc_step<DIV, SM>(e, m, s_tab, sym);
+  if (act) rare = enc_step<DIV, SM>(e, m, t);
   if (__builtin_expect(__any((int)rare), 0)) {
     if (rare) enc_rare(e);
     enc_flush(e, lane, wring, wout);
   }
 }
 
-// 8 symbols from two dwords, then a flush check (wave-uniform)
-template <int DIV, int SM>
-static __device__ __forceinline__ void enc8(Enc& e, const ModelArgs& m, const uint2* s_tab,
-                                            u32 w0, u32 w1, bool act, u32 lane,
-                                            const u32* wring, const EncOut* wout) {
-  enc_sym<DIV, SM>(e, m, s_tab, w0 & 255u, act, lane, wring, wout);
-  enc_sym<DIV, SM>(e, m, s_tab, (w0 >> 8) & 255u, act, lane, wring, wout);
-  enc_sym<DIV, SM>(e, m, s_tab, (w0 >> 16) & 255u, act, lane, wring, wout);
-  enc_sym<DIV, SM>(e, m, s_tab, w0 >> 24, act, lane, wring, wout);
-  enc_sym<DIV, SM>(e, m, s_tab, w1 & 255u, act, lane, wring, wout);
-  enc_sym<DIV, SM>(e, m, s_tab, (w1 >> 8) & 255u, act, lane, wring, wout);
-  enc_sym<DIV, SM>(e, m, s_tab, (w1 >> 16) & 255u, act, lane, wring, wout);
-  enc_sym<DIV, SM>(e, m, s_tab, w1 >> 24, act, lane, wring, wout);
-  enc_flush(e, lane, wring, wout);
-}
-
+// 16 symbols from one 16-B load, a flush check after every 8 (wave-uniform).  The table entry
+// of the next symbol is read before the current symbol is coded, so the LDS latency is off the
+// range -> range dependency chain.
 template <int DIV, int SM>
 static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const uint2* s_tab,
                                              uint4 v, bool act, u32 lane, const u32* wring,
                                              const EncOut* wout) {
-  enc8<DIV, SM>(e, m, s_tab, v.x, v.y, act, lane, wring, wout);
-  enc8<DIV, SM>(e, m, s_tab, v.z, v.w, act, lane, wring, wout);
+  const u32 w[4] = {v.x, v.y, v.z, v.w};
+  uint2 t = s_tab[w[0] & 255u];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    uint2 tn = t;
+    if (i < 15) tn = s_tab[(w[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 255u];
+    enc_sym<DIV, SM>(e, m, t, act, lane, wring, wout);
+    t = tn;
+    if ((i & 7) == 7) enc_flush(e, lane, wring, wout);
+  }
 }
 
 // one symbol fetched byte-wise (unaligned head / tail of a chunk)
@@ -248,7 +261,7 @@ static __device__ __forceinline__ void enc_byte_sym(Enc& e, const ModelArgs& m,
                                                     bool act, u32 lane, const u32* wring,
                                                     const EncOut* wout) {
   const u32 sym = act ? (u32)sp[i] : 0u;
-  enc_sym<DIV, SM>(e, m, s_tab, sym, act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab[sym], act, lane, wring, wout);
 }
 
 // the first symbol of a chunk the reference cannot encode (rare: flagged chunks only)
@@ -307,8 +320,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   e.low = 0;  // RangeCoder::default (range_coder.rs:13-20)
   e.range = ~0ull;
   e.acc = 0;
-  e.nbits = 8 * (a & 3);  // pad bytes in front of the slot (never stored)
-  e.wpos = a & ~3u;
+  e.B = 8 * a;  // pad bytes in front of the slot (never stored)
   e.fpos = 0;
   e.err = 0;
   e.ring = s_ring + wave * ENC_RING * 64 + lane;
@@ -317,39 +329,60 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   u64 head = (64 - ((uintptr_t)sp & 63)) & 63;  // symbols before the first 64-B aligned tile
   if (head > n) head = n;
   const u64 ntile = (n - head) >> 6;
-  const u64 tail0 = head + (ntile << 6);
   // head: byte-wise, all lanes in step (flush rounds are wave-wide)
   for (u64 i = 0; __any((int)(i < head)); ++i) {
     enc_byte_sym<DIV, SM>(e, m, s_tab, sp, i, i < head, lane, wring, wout);
     if ((i & 7) == 7) enc_flush(e, lane, wring, wout);
   }
-  // body: 64-symbol tiles, the next one prefetched
-  const uint4* tp = reinterpret_cast<const uint4*>(sp + head);
+  // body, part 1: the tiles every live lane of the wave has, with every lane active (no
+  // per-symbol exec masking).  Dead lanes run along on a dummy tile (g_sink, zeros) and a slot
+  // with no writable bytes; their results are dropped.
+  u64 tm = live ? ntile : ~0ull;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const u64 v = ((u64)(u32)__shfl_xor((int)hi32(tm), o) << 32) | (u32)__shfl_xor((int)(u32)tm, o);
+    tm = v < tm ? v : tm;
+  }
+  if (tm == ~0ull) tm = 0;  // no live lane in this wave
+  const u64 tmin = ((u64)__builtin_amdgcn_readfirstlane(hi32(tm)) << 32) |
+                   __builtin_amdgcn_readfirstlane((u32)tm);  // wave-uniform (scalar) trip count
+  const uint4* tp = live ? reinterpret_cast<const uint4*>(sp + head)
+                         : reinterpret_cast<const uint4*>(g_sink);
+  const u64 tstep = live ? 4 : 0;  // uint4s per tile
   uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0;
-  if (ntile) {
+  if (tmin) {
     c0 = tp[0];
     c1 = tp[1];
     c2 = tp[2];
     c3 = tp[3];
   }
-  for (u64 t = 0; __any((int)(t < ntile)); ++t) {
-    const bool act = t < ntile;
+  for (u64 t = 0; t < tmin; ++t) {
     uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
-    if (t + 1 < ntile) {
-      n0 = tp[(t + 1) * 4 + 0];
-      n1 = tp[(t + 1) * 4 + 1];
-      n2 = tp[(t + 1) * 4 + 2];
-      n3 = tp[(t + 1) * 4 + 3];
+    if (t + 1 < tmin) {
+      const uint4* q = tp + (t + 1) * tstep;
+      n0 = q[0];
+      n1 = q[1];
+      n2 = q[2];
+      n3 = q[3];
     }
-    enc16<DIV, SM>(e, m, s_tab, c0, act, lane, wring, wout);
-    enc16<DIV, SM>(e, m, s_tab, c1, act, lane, wring, wout);
-    enc16<DIV, SM>(e, m, s_tab, c2, act, lane, wring, wout);
-    enc16<DIV, SM>(e, m, s_tab, c3, act, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c0, true, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c1, true, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c2, true, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c3, true, lane, wring, wout);
     c0 = n0;
     c1 = n1;
     c2 = n2;
     c3 = n3;
   }
+  // body, part 2 (ragged waves): the remaining 16-symbol blocks of the tiles, lanes masked
+  const u64 nblk = ntile * 4;
+  for (u64 b = tmin * 4; __any((int)(b < nblk)); ++b) {
+    const bool act = b < nblk;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (act) v = tp[b];
+    enc16<DIV, SM>(e, m, s_tab, v, act, lane, wring, wout);
+  }
+  const u64 tail0 = head + (ntile << 6);
   for (u64 j = 0; __any((int)(tail0 + j < n)); ++j) {  // j is wave-uniform
     enc_byte_sym<DIV, SM>(e, m, s_tab, sp, tail0 + j, tail0 + j < n, lane, wring, wout);
     if ((j & 7) == 7) enc_flush(e, lane, wring, wout);
@@ -361,15 +394,17 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
     enc_emit_byte(e, (u32)(e.low >> 56));
     e.low <<= 8;
   }
-  const u32 len = e.wpos + (e.nbits >> 3) - a;
-  if (e.nbits) {
-    e.ring[((e.wpos >> 2) & (ENC_RING - 1)) * 64] = __builtin_bswap32((u32)(e.acc << (32 - e.nbits)));
-    e.wpos += 4;
+  const u32 len = (e.B >> 3) - a;
+  u32 wend = enc_wpos(e);
+  if (e.B & 31) {  // the last, incomplete dword
+    e.ring[((e.B >> 5) & (ENC_RING - 1)) * 64] =
+        __builtin_bswap32((u32)(e.acc << (32 - (e.B & 31))));
+    wend += 4;
   }
   // final rounds: the last (partial) units, clipped to the stream end
   const u32 end = a + len;
   if (end < s_out[tid].hi_ok) s_out[tid].hi_ok = end;
-  while (__any((int)(e.fpos < e.wpos))) enc_round(e, e.fpos < e.wpos, lane, wring, wout);
+  while (__any((int)(e.fpos < wend))) enc_round(e, e.fpos < wend, lane, wring, wout);
   if (live) {
     if (SM) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
     if (!e.err && (u64)len > cap) e.err = RC_F_CAPACITY;
@@ -505,41 +540,68 @@ static __device__ __forceinline__ float cvt_f32(u32 v) {
   return f;
 }
 
+// float -> u32 as the single instruction, which saturates (negative -> 0, >= 2^32 -> 2^32 - 1)
+static __device__ __forceinline__ u32 cvt_u32_sat(float f) {
+  u32 v;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(v) : "v"(f));
+  return v;
+}
+
+// code bytes a symbol may consume before the next ring check: SM checks once per 4 symbols
+// (<= 3 bytes each), otherwise every symbol (<= 7 bytes)
+#define DEC_NEED_SM 12u
+#define DEC_NEED_WIDE 8u
+
 template <int DIV, int SM, int LUT>
 static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const uint2* s_tab,
                                               const u32* s_lut) {
-  // the code bytes at cpos (the ring holds >= 4 of them, >= 8 when !SM): the ones this
-  // symbol settles are shifted into x at the end
+  // the code bytes at cpos (the ring holds the ones this symbol can settle); they are shifted
+  // into x at the end
   const u32* rp = d.ring + ((d.cpos >> 2) & (DEC_RING - 1)) * 64;
   const u32 D0 = rp[0], D1 = rp[64];
   const u32 D2 = SM ? 0u : rp[128];
   const u64 x = d.x;
   const u64 r = range_par_total<DIV>(d.range, m);
-  // hint q ~ x / r ~ x * total / range from the top 32 bits of x and range, both shifted by
-  // clz(range) (range >= 2^48, so the shift is < 16); relative error ~2^-22
-  const u32 e = (u32)__builtin_clz(hi32(d.range));
-  const float X = cvt_f32(hi32(x << e)), R = cvt_f32(hi32(d.range << e));
-  const float qf = fminf(X * (m.ftotal * __builtin_amdgcn_rcpf(R)), 4.0e9f);
-  const u32 qh = (u32)qf;
+  // hint q ~ x / r ~ x * total / range from the top 32 bits of x and range.  Direct tables
+  // (total <= 2048) take the high halves as they are: range >= 2^48, so the relative error is
+  // <= 2^-15 (and ~2^-24 for the usual range >= 2^56), far inside one frequency step.  Bucket
+  // tables (totals up to 2^32) first shift both by clz(range), for a relative error ~2^-22.
+  float X, R;
+  if (LUT) {
+    X = cvt_f32(hi32(x));
+    R = cvt_f32(hi32(d.range));
+  } else {
+    const u32 e = (u32)__builtin_clz(hi32(d.range));
+    X = cvt_f32(hi32(x << e));
+    R = cvt_f32(hi32(d.range << e));
+  }
+  // The table index is masked, not clamped: the tables are padded to a power of two with valid
+  // entries, so an out-of-range hint (corrupt streams, x >= range; or rounding to q == total)
+  // only starts the exact fix-up below from another symbol, whose result does not depend on
+  // where it starts.  (A v_mul_f32 clamp modifier was tried instead and gave wrong hints.)
+  const float rR = __builtin_amdgcn_rcpf(R);
   u32 s;
   uint2 t;
-  if (LUT) {  // direct table: candidate symbol and its (cum, c) in one LDS read
-    const u32 ent = s_lut[min(qh, m.total - 1)];
+  if (LUT) {  // direct table: candidate symbol and its (cum, c) in one LDS read at byte 4q
+    const u32 q4 = cvt_u32_sat(X * ((4.0f * m.ftotal) * rR)) & (m.lut_max << 2);
+    const u32 ent = *reinterpret_cast<const u32*>(reinterpret_cast<const char*>(s_lut) + q4);
     s = ent & 255u;
     t = make_uint2((ent >> 8) & 0xFFFu, ent >> 20);
   } else {  // bucket table, then the (cum, c) table
-    const u32 b = min(qh >> m.lut_shift, m.lut_max);
+    const u32 qh = cvt_u32_sat(X * (m.ftotal * rR));
+    const u32 b = (qh >> m.lut_shift) & m.lut_max;
     const u32 ent = s_lut[b];
     s = ((qh - (b << m.lut_shift)) >= (ent >> 16)) ? ((ent >> 8) & 255u) : (ent & 255u);
     t = s_tab[s];
   }
   u64 A = mul_rv<SM>(r, t.x);
   u64 B = mul_rv<SM>(r, t.y);
-  // exact verification r*cum[s] <= x < r*cum[s+1]; the hint is rarely off.  (At s = n - 1 the
-  // upper test fails only on corrupt input, x >= r * total: dec_fix keeps s = n - 1 there.)
-  const bool off = (A > x) | (x - A >= B);
-  if (__builtin_expect(__any((int)off), 0)) {
-    if (off) {
+  // exact verification r*cum[s] <= x < r*cum[s+1] as ONE unsigned test: A + B <= range < 2^64,
+  // so when A > x the wrapped difference x - A is >= 2^64 - A > B.  The hint is rarely off.
+  // (At s = n - 1 the test fails only on corrupt input, x >= r * total: dec_fix keeps s = n-1.)
+  u64 dx = x - A;
+  if (__builtin_expect(__any((int)(dx >= B)), 0)) {
+    if (dx >= B) {
       dec_fix(s, t, A, B, x, r, s_tab, m.n);
       // the tables only hold symbols with c > 0, so c == 0 can only come from dec_fix: corrupt
       // input (the reference loops forever); an over-read, if any, came first
@@ -547,36 +609,50 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
         d.err = d.err ? d.err : (d.cpos > d.lim ? RC_F_TRUNCATED : RC_F_CORRUPT);
         B = r;
       }
+      dx = x - A;
     }
   }
   // param_update (range_coder.rs:53-92)
   d.low += A;
   d.range = B;
-  const u64 xx = d.low ^ (d.low + d.range);
-  const u32 k8 = SM ? ((u32)__builtin_clz(hi32(xx)) & 24u) : ((u32)__clzll(xx) & 56u);
+  // closed-form no_carry_expansion; SM: range >= 2^32 here, so the high halves
+  // differ and k8 <= 24
+  const u32 k8 = SM ? (ffbh(hi32(d.low) ^ hi32(d.low + d.range)) & 24u)
+                    : ((u32)__clzll(d.low ^ (d.low + d.range)) & 56u);
   d.low <<= k8;
   d.range <<= k8;
-  // data' = data << k8 | k settled bytes, low' = (low + A) << k8, so
-  // x' = ((x - A) << k8) | those bytes (shift_left_buffer, decoder.rs:31-35)
-  const u32 sh = d.cpos & 3;
-  const u32 b0 = __builtin_bswap32(__builtin_amdgcn_alignbyte(D1, D0, sh));
-  u32 nb;
+  // data' = data << k8 | k settled bytes and low' = (low + A) << k8, so x' = ((x - A) << k8) |
+  // those bytes (shift_left_buffer, decoder.rs:31-35): the high half of dx << k8, and the high
+  // half of (dx_lo : next 4 code bytes) << k8 (alignbyte uses cpos & 3 only)
+  const u32 w0 = __builtin_bswap32(__builtin_amdgcn_alignbyte(D1, D0, d.cpos));
   if (SM) {  // k8 <= 24
-    nb = hi32((u64)b0 << k8);
+    const u32 xh = hi32(dx << k8);
+    const u32 xl = hi32((((u64)(u32)dx) << 32 | w0) << k8);
+    d.x = ((u64)xh << 32) | xl;
   } else {   // k8 <= 56
-    const u64 b = ((u64)b0 << 32) | __builtin_bswap32(__builtin_amdgcn_alignbyte(D2, D1, sh));
-    nb = 0;
-    d.x = k8 ? b >> (64 - k8) : 0ull;
+    const u64 b = ((u64)w0 << 32) | __builtin_bswap32(__builtin_amdgcn_alignbyte(D2, D1, d.cpos));
+    d.x = (dx << k8) | (k8 ? b >> (64 - k8) : 0ull);
   }
-  d.x = SM ? (((x - A) << k8) | nb) : (((x - A) << k8) | d.x);
-  d.cpos += k8 >> 3;
-  // rare: range_reduction_expansion, or the ring runs short for the next symbol
-  const u32 need = SM ? 4u : 8u;
-  const bool rare = (hi32(d.range) < 0x10000u) | ((int)(d.fill - d.cpos) < (int)need);
+  u32 nbytes;  // k8 >> 3 as a plain shift (the compiler's v_bfe from the ffbh result costs more)
+  asm("v_lshrrev_b32 %0, 3, %1" : "=v"(nbytes) : "v"(k8));
+  d.cpos += nbytes;
+  // rare: range_reduction_expansion, or (wide models) the ring runs short for the next symbol
+  const bool rare = SM ? (hi32(d.range) < 0x10000u)
+                       : ((hi32(d.range) < 0x10000u) | ((int)(d.fill - d.cpos) < (int)DEC_NEED_WIDE));
   if (__builtin_expect(__any((int)rare), 0)) {
-    if (rare) dec_rare(d, need);
+    if (rare) dec_rare(d, SM ? DEC_NEED_SM : DEC_NEED_WIDE);
   }
   return s;
+}
+
+// SM models: the ring check for the next 4 symbols (wave-uniform call sites)
+template <int SM>
+static __device__ __forceinline__ void dec_check4(Dec& d) {
+  if (!SM) return;
+  const bool low = (int)(d.fill - d.cpos) < (int)DEC_NEED_SM;
+  if (__builtin_expect(__any((int)low), 0)) {
+    if (low) dec_sync(d, DEC_NEED_SM);
+  }
 }
 
 template <int DIV, int SM, int LUT>
@@ -627,7 +703,11 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   u64 i = 0;
   u64 head = (16 - ((uintptr_t)op & 15)) & 15;
   if (head > n) head = n;
-  for (; i < head; ++i) op[i] = (uint8_t)dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut);
+  dec_check4<SM>(d);
+  for (; i < head; ++i) {
+    op[i] = (uint8_t)dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut);
+    dec_check4<SM>(d);
+  }
   // body: 16-symbol phases: store decoded block, commit pending load, maybe issue the next
   const u64 nph = (n - i) >> 4;
   uint4* ob = reinterpret_cast<uint4*>(op + i);
@@ -637,12 +717,17 @@ __global__ __launch_bounds__(WG) void k_decode_static(
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) w[q] |= dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut) << (8 * j);
+      if (q < 3) dec_check4<SM>(d);
     }
     ob[b] = make_uint4(w[0], w[1], w[2], w[3]);
     dec_phase(d);
+    dec_check4<SM>(d);
   }
   i += nph << 4;
-  for (; i < n; ++i) op[i] = (uint8_t)dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut);
+  for (; i < n; ++i) {
+    op[i] = (uint8_t)dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut);
+    dec_check4<SM>(d);
+  }
   // shift_left_buffer panics once more bytes are needed than the stream holds (decoder.rs:33)
   if (!d.err && d.cpos > d.lim) d.err = RC_F_TRUNCATED;
   flags[k] = d.err;
@@ -877,6 +962,9 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
     }
     lut[b] = s | (s1 << 8) | (split << 16);
   }
+  // pad to a power of two (the kernel masks the bucket index) with the last bucket
+  while (lut.size() & (lut.size() - 1)) lut.push_back(lut.back());
+  a.lut_max = (u32)lut.size() - 1;
 
   if (total_freq <= 2048) {  // direct table: q -> s | cum << 8 | c << 20
     a.direct = 1;
@@ -888,6 +976,8 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
       while (sym + 1 < n_symbols && cum_freq[sym + 1] <= q) ++sym;
       lut[q] = sym | (cum_freq[sym] << 8) | (c_freq[sym] << 20);
     }
+    while (lut.size() & (lut.size() - 1)) lut.push_back(lut.back());  // pow2 (masked index)
+    a.lut_max = (u32)lut.size() - 1;
   }
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
@@ -958,11 +1048,16 @@ rc_status rc_encode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
 #define RC_ENC_LAUNCH(D, S)                                                                \
   hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, ctx->cur, m->args, syms,    \
                      sym_off, n_chunks, out, out_off, out_len, flags)
+#ifdef RC_DEV_ONLY  // scratch builds for kernel tuning: the headline variants only
+  if (m->div != DIV_POW2 || !sm) return RC_E_ARG;
+  RC_ENC_LAUNCH(DIV_POW2, 1);
+#else
   if (m->div == DIV_POW2) {
     if (sm) RC_ENC_LAUNCH(DIV_POW2, 1); else RC_ENC_LAUNCH(DIV_POW2, 0);
   } else {
     if (sm) RC_ENC_LAUNCH(DIV_MAGIC, 1); else RC_ENC_LAUNCH(DIV_MAGIC, 0);
   }
+#endif
 #undef RC_ENC_LAUNCH
   return launch_status();
 }
@@ -988,6 +1083,10 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
                      code, code_off, code_len, syms_out, sym_off, n_chunks, flags)
   const bool dl = m->args.direct != 0;
   const size_t lut_bytes = (size_t)(m->args.lut_max + 1) * sizeof(u32);
+#ifdef RC_DEV_ONLY
+  if (m->div != DIV_POW2 || !sm) return RC_E_ARG;
+  if (dl) RC_DEC_LAUNCH(DIV_POW2, 1, 1); else RC_DEC_LAUNCH(DIV_POW2, 1, 0);
+#else
   if (m->div == DIV_POW2) {
     if (sm) { if (dl) RC_DEC_LAUNCH(DIV_POW2, 1, 1); else RC_DEC_LAUNCH(DIV_POW2, 1, 0); }
     else    { if (dl) RC_DEC_LAUNCH(DIV_POW2, 0, 1); else RC_DEC_LAUNCH(DIV_POW2, 0, 0); }
@@ -995,6 +1094,7 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
     if (sm) { if (dl) RC_DEC_LAUNCH(DIV_MAGIC, 1, 1); else RC_DEC_LAUNCH(DIV_MAGIC, 1, 0); }
     else    { if (dl) RC_DEC_LAUNCH(DIV_MAGIC, 0, 1); else RC_DEC_LAUNCH(DIV_MAGIC, 0, 0); }
   }
+#endif
 #undef RC_DEC_LAUNCH
   return launch_status();
 }
