@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--config", choices=["uniform", "zipf"], default="uniform")
     p.add_argument("--no-zipf", action="store_true", help="skip the secondary Zipf leg")
     p.add_argument("--no-adaptive", action="store_true", help="skip the adaptive (C4) leg")
+    p.add_argument("--no-model-build", action="store_true",
+                   help="skip the histogram / entropy-report leg (on the Zipf inputs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU sample wall time")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
@@ -143,6 +145,41 @@ def run_leg(torch, dist, leg, steps, warmup, world):
           and equal_chunked(torch, leg.dec, leg.syms))
     code_bytes = int(leg.out_len.sum())
     return dict(t=t, enc_ms=enc_ms, dec_ms=dec_ms, ok=ok, code_bytes=code_bytes)
+
+
+def model_build_leg(torch, rc, leg, code_bytes, reps=3):
+    """SURVEY.md §8f rows 2 and 4 on the leg's inputs: GPU histogram (batch + per-chunk rows),
+    its HBM roofline (reads 1 B/symbol, writes 1 KiB per chunk), the table it yields, and the
+    entropy report: ideal code length of the leg's model against the coded bytes."""
+    n, L = leg.n, leg.L
+    _, ch = rc.histogram(leg.syms, leg.sym_off, per_chunk=True)  # warm-up
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    hist = None
+    for e0, e1 in ev:
+        e0.record()
+        hist, ch = rc.histogram(leg.syms, leg.sym_off, per_chunk=True)
+        e1.record()
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    alg = n * L + n * 256 * 4
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    bits = rc.ideal_bits(leg.model, ch)
+    t1.record()
+    torch.cuda.synchronize()
+    counts = hist.cpu().numpy().astype(np.uint64)
+    c, cum, total = rc.quantize_counts(counts, 1 << 16, all_symbols=True)
+    ideal = float(bits.sum().item())
+    return dict(
+        histogram_ms=round(ms, 3), histogram_gbps=round(alg / ms / 1e6, 1),
+        histogram_roofline_frac=round(alg / ms / 1e6 / HBM_PEAK_GBPS, 4),
+        ideal_bits_ms=round(t0.elapsed_time(t1), 3),
+        ideal_bits_per_symbol=round(ideal / (n * L), 5),
+        coded_bits_per_symbol=round(code_bytes * 8 / (n * L), 5),
+        coding_overhead_bits_per_symbol=round((code_bytes * 8 - ideal) / (n * L), 6),
+        built_table_total=total, built_table_max_c=int(c.max()), built_table_min_c=int(c.min()))
 
 
 def cpu_baseline(torch, leg, seconds, threads):
@@ -248,6 +285,8 @@ def main():
             roofline_frac_encode=round(zb / zr["enc_ms"] / 1e6 / HBM_PEAK_GBPS, 4),
             roofline_frac_decode=round(zb / zr["dec_ms"] / 1e6 / HBM_PEAK_GBPS, 4),
             bit_exact_round_trip=zr["ok"])
+        if not args.no_model_build:
+            extras["model_build"] = model_build_leg(torch, rc, z, zr["code_bytes"])
     if not args.no_adaptive and args.config == "uniform" and L % 16384 == 0:
         La = 16384
         na = n * (L // La)

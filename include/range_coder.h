@@ -137,6 +137,38 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
 rc_status rc_synth_fill(rc_ctx* ctx, uint64_t seed, const uint8_t* inv_cdf_host,
                         uint8_t* syms_dev, uint64_t chunk_len, uint32_t n_chunks);
 
+/* ---- model construction: the step before encode ----
+ * The reference builds a FreqTable by counting symbols (FreqTable::new + add_alphabet_freq per
+ * symbol, examples/sample_impl.rs:49-60) and then scanning (calc_cum, :61-69).              */
+
+/* Symbol histogram of n_chunks chunks (device pointers; stream-ordered).
+ * chunk_hist_dev  NULL or n_chunks*256 uint32: row k = counts of chunk k (overwritten)
+ * hist_dev        NULL or 256 uint64: batch counts ADDED into it (zero it first)          */
+rc_status rc_histogram(rc_ctx* ctx, const uint8_t* syms_dev, const uint64_t* sym_off_dev,
+                       uint32_t n_chunks, uint32_t* chunk_hist_dev, uint64_t* hist_dev);
+
+/* Counts -> (c, cum, total) table (host only, no device needed).
+ * target_total == 0: calc_cum's exact table, c = counts (total must stay < 2^32; with
+ * RC_Q_ALL_SYMBOLS absent symbols get c = 1);
+ * otherwise c_i = max(1, round(counts_i * T / sum)) for modelled symbols, the difference to T
+ * folded into the largest entry (deficit; lowest index on ties) or taken from the largest
+ * entries first, never below 1 (excess).  Modelled symbols: counts_i > 0, or every symbol
+ * with RC_Q_ALL_SYMBOLS (so symbols absent from the sample stay encodable).
+ * Returns RC_E_BAD_MODEL when no table exists (T below the number of modelled symbols, an
+ * empty sample without RC_Q_ALL_SYMBOLS, a total >= 2^32).                                  */
+#define RC_Q_ALL_SYMBOLS 1u
+rc_status rc_quantize_counts(const uint64_t* counts_host, uint32_t n_symbols,
+                             uint64_t target_total, uint32_t qflags, uint32_t* c_out_host,
+                             uint32_t* cum_out_host, uint32_t* total_out_host);
+
+/* Batched PModel::ideal_code_length (pmodel.rs:14-40): bits_dev[k] = sum over symbols s of
+ * chunk k of log2(total / c[s]) = sum_i hist[k][i] * (ln total - ln c_i) / ln 2, in f64,
+ * from rc_histogram's chunk rows.  A symbol with c == 0 (no code length in the reference)
+ * makes its chunk's sum +inf.  Synchronous with respect to the host table.                 */
+rc_status rc_ideal_bits(rc_ctx* ctx, const uint32_t* c_freq_host, uint32_t n_symbols,
+                        uint32_t total_freq, const uint32_t* chunk_hist_dev, uint32_t n_chunks,
+                        double* bits_dev);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,5 +7,6 @@ from .api import (  # noqa: F401
     slot_capacity,
 )
 from . import synth  # noqa: F401
+from .model_build import build_model, histogram, ideal_bits, quantize_counts  # noqa: F401
 
 __version__ = "0.1.0"

@@ -28,8 +28,9 @@ EXPORTS = (
     "rc_ctx_synchronize",
     "rc_status_string", "rc_last_error", "rc_device_info", "rc_model_create_static",
     "rc_model_create_adaptive", "rc_model_destroy", "rc_encode_batch", "rc_decode_batch", "rc_encode_host",
-    "rc_decode_host", "rc_synth_fill",
+    "rc_decode_host", "rc_synth_fill", "rc_histogram", "rc_quantize_counts", "rc_ideal_bits",
 )
+Q_ALL_SYMBOLS = 1
 
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
@@ -74,6 +75,9 @@ def load():
     L.rc_encode_host.argtypes = [_P, _P, _P, _P, _U32, _P, _P, _P, _P]
     L.rc_decode_host.argtypes = [_P, _P, _P, _P, _P, _P, _P, _U32, _P]
     L.rc_synth_fill.argtypes = [_P, _U64, _P, _P, _U64, _U32]
+    L.rc_histogram.argtypes = [_P, _P, _P, _U32, _P, _P]
+    L.rc_quantize_counts.argtypes = [_P, _U32, _U64, _U32, _P, _P, _P]
+    L.rc_ideal_bits.argtypes = [_P, _P, _U32, _U32, _P, _U32, _P]
     for name in EXPORTS:
         if name not in ("rc_status_string", "rc_last_error"):
             getattr(L, name).restype = _I

@@ -896,6 +896,15 @@ rc_status rc_ctx_destroy(rc_ctx* ctx) {
   return RC_OK;
 }
 
+// internal (not in the header): the context's device and current stream, for the other
+// translation units of the library
+rc_status rc_ctx_stream_(rc_ctx* ctx, hipStream_t* s, int* device) {
+  if (!ctx || !s || !device) return RC_E_ARG;
+  *s = ctx->cur;
+  *device = ctx->device;
+  return RC_OK;
+}
+
 rc_status rc_ctx_set_stream(rc_ctx* ctx, void* hip_stream) {
   if (!ctx) return RC_E_ARG;
   ctx->cur = (hipStream_t)hip_stream;

@@ -1,0 +1,240 @@
+// rc_model_build.hip — the step before encode: building the frequency table from the data, on
+// the GPU.
+//
+// The reference builds its model on the CPU, one symbol at a time: FreqTable::new, then
+// add_alphabet_freq per symbol (examples/sample_impl.rs:49-60), then calc_cum's exclusive scan
+// (:61-69).  Here:
+//   * k_histogram counts symbols of many chunks at once (per-chunk and/or batch histograms):
+//     pure HBM streaming, 16-B loads, LDS sub-histograms;
+//   * rc_quantize_counts turns counts into a (c, cum, total) table: exactly calc_cum's table
+//     when no target is given, or a table scaled to a target total (e.g. 2^16, so the coder
+//     takes its fast power-of-two path), deterministic and restated by the oracle;
+//   * k_ideal_bits is the batched PModel::ideal_code_length (pmodel.rs:14-40): per chunk,
+//     sum over its histogram of count * log2(total / c), in f64.
+#include "rc_common.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#define HWG 256
+#define HCOPIES 4  // sub-histograms per wave, interleaved per bin: lanes L, L+1, L+2, L+3 that
+                   // hit one symbol land in 4 different banks
+
+// chunk-stride grid: each WG counts whole chunks into LDS, flushes each chunk's 256 counts
+// (chunk_hist, optional) and accumulates its bins in registers for one final global atomic
+// per bin (hist, optional)
+__global__ __launch_bounds__(HWG) void k_histogram(const uint8_t* __restrict__ syms,
+                                                   const u64* __restrict__ sym_off,
+                                                   u32 n_chunks, u32* __restrict__ chunk_hist,
+                                                   u64* __restrict__ hist) {
+  __shared__ u32 sh[(HWG / 64) * 256 * HCOPIES];
+  const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  u32* my = sh + wave * 256 * HCOPIES + (lane & (HCOPIES - 1));
+  RC_VGPR_FLOOR_64();
+  u64 acc = 0;  // bin tid over this WG's chunks
+  for (u32 k = blockIdx.x; k < n_chunks; k += gridDim.x) {
+    for (u32 j = tid; j < (HWG / 64) * 256 * HCOPIES; j += HWG) sh[j] = 0;
+    __syncthreads();
+    const u64 s0 = sym_off[k], n = sym_off[k + 1] - s0;
+    const uint8_t* p = syms + s0;
+    u64 head = (16 - ((uintptr_t)p & 15)) & 15;
+    if (head > n) head = n;
+    if (tid < head) atomicAdd(&my[(u32)p[tid] * HCOPIES], 1u);
+    const u64 nv = (n - head) >> 4;
+    const u32x4* v = reinterpret_cast<const u32x4*>(p + head);
+#pragma unroll 4
+    for (u64 i = tid; i < nv; i += HWG) {
+      const u32x4 w = gload16(v + i);
+      const u32 ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) atomicAdd(&my[((ws[q] >> (8 * b)) & 255u) * HCOPIES], 1u);
+      }
+    }
+    for (u64 i = head + (nv << 4) + tid; i < n; i += HWG) atomicAdd(&my[(u32)p[i] * HCOPIES], 1u);
+    __syncthreads();
+    u32 cnt = 0;
+#pragma unroll
+    for (u32 w = 0; w < HWG / 64; ++w) {
+#pragma unroll
+      for (u32 c = 0; c < HCOPIES; ++c) cnt += sh[w * 256 * HCOPIES + tid * HCOPIES + c];
+    }
+    if (chunk_hist) chunk_hist[(u64)k * 256 + tid] = cnt;
+    acc += cnt;
+    __syncthreads();
+  }
+  if (hist && acc) atomicAdd(reinterpret_cast<unsigned long long*>(hist + tid), (unsigned long long)acc);
+}
+
+// per chunk: bits = sum_i hist[i] * icl[i] in f64, bins in order 0..255 (icl[i] = +inf for
+// c_i == 0: the reference's ideal_code_length returns Err there, pmodel.rs:16-18).  One thread
+// per chunk; the histogram rows are read through LDS in 256-chunk tiles (coalesced).
+__global__ __launch_bounds__(HWG) void k_ideal_bits(const double* __restrict__ icl,
+                                                    const u32* __restrict__ chunk_hist,
+                                                    u32 n_chunks, double* __restrict__ bits) {
+  __shared__ double s_icl[256];
+  __shared__ u32 s_h[HWG][33];  // 32 bins at a time, padded row
+  const u32 tid = threadIdx.x;
+  RC_VGPR_FLOOR_32();
+  s_icl[tid] = icl[tid];
+  const u32 k0 = blockIdx.x * HWG;
+  double acc = 0.0;
+  for (u32 b0 = 0; b0 < 256; b0 += 32) {
+    __syncthreads();
+    // tile: chunk k0 + r, bins b0 .. b0+31; thread t loads (r, c) = (j / 32, j % 32)
+    for (u32 j = tid; j < HWG * 32; j += HWG) {
+      const u32 r = j >> 5, c = j & 31;
+      s_h[r][c] = (k0 + r < n_chunks) ? chunk_hist[(u64)(k0 + r) * 256 + b0 + c] : 0u;
+    }
+    __syncthreads();
+    for (u32 c = 0; c < 32; ++c) {
+      const u32 h = s_h[tid][c];
+      if (h) acc = fma((double)h, s_icl[b0 + c], acc);
+    }
+  }
+  if (k0 + tid < n_chunks) bits[k0 + tid] = acc;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------
+struct rc_ctx;  // rc_kernels.hip
+extern "C" {
+rc_status rc_ctx_stream_(rc_ctx* ctx, hipStream_t* s, int* device);  // rc_kernels.hip
+}
+
+namespace {
+struct DevSet {
+  int prev = -1;
+  explicit DevSet(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DevSet() {
+    int now = -1;
+    if (prev >= 0 && hipGetDevice(&now) == hipSuccess && now != prev) (void)hipSetDevice(prev);
+  }
+};
+}  // namespace
+
+extern "C" {
+
+rc_status rc_histogram(rc_ctx* ctx, const uint8_t* syms, const uint64_t* sym_off,
+                       uint32_t n_chunks, uint32_t* chunk_hist, uint64_t* hist) {
+  hipStream_t s;
+  int dev;
+  if (rc_ctx_stream_(ctx, &s, &dev) != RC_OK || n_chunks > RC_MAX_CHUNKS) return RC_E_ARG;
+  if (n_chunks == 0 || (!chunk_hist && !hist)) return RC_OK;
+  if (!syms || !sym_off) return RC_E_ARG;
+  DevSet g(dev);
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return RC_E_DEVICE;
+  const u32 grid = std::min<u32>(n_chunks, (u32)cus * 8);  // 16 KiB LDS/WG: 8 WGs per CU
+  hipLaunchKernelGGL(k_histogram, dim3(grid), dim3(HWG), 0, s, syms, sym_off, n_chunks,
+                     chunk_hist, hist);
+  return hipGetLastError() == hipSuccess ? RC_OK : RC_E_DEVICE;
+}
+
+rc_status rc_quantize_counts(const uint64_t* counts, uint32_t n_symbols, uint64_t target_total,
+                             uint32_t qflags, uint32_t* c_out, uint32_t* cum_out,
+                             uint32_t* total_out) {
+  if (!counts || !c_out || !cum_out || !total_out || n_symbols < 1 || n_symbols > 256)
+    return RC_E_ARG;
+  const bool all = (qflags & RC_Q_ALL_SYMBOLS) != 0;
+  std::vector<u64> c(n_symbols);
+  unsigned __int128 N = 0;
+  for (u32 i = 0; i < n_symbols; ++i) N += counts[i];
+  if (target_total == 0) {  // exact FreqTable: c = counts, total = sum (sample_impl.rs:58-69)
+    for (u32 i = 0; i < n_symbols; ++i) c[i] = counts[i] + ((all && counts[i] == 0) ? 1u : 0u);
+  } else {
+    u32 need = 0;
+    for (u32 i = 0; i < n_symbols; ++i) need += (all || counts[i] > 0) ? 1u : 0u;
+    if (N == 0) {
+      if (!all) return RC_E_BAD_MODEL;  // nothing to model
+      need = n_symbols;
+    }
+    if (target_total < need || target_total > 0xFFFFFFFFull) return RC_E_BAD_MODEL;
+    // c_i = max(1, round(counts_i * T / N)) for modelled symbols (half rounds up)
+    u64 sum = 0;
+    for (u32 i = 0; i < n_symbols; ++i) {
+      if (N == 0) {
+        c[i] = 1;
+      } else if (counts[i] == 0 && !all) {
+        c[i] = 0;
+      } else {
+        const unsigned __int128 q = ((unsigned __int128)counts[i] * target_total + N / 2) / N;
+        c[i] = q < 1 ? 1 : (u64)q;
+      }
+      sum += c[i];
+    }
+    // fold the difference: a deficit goes to the largest entry (lowest index on ties); an
+    // excess is taken from the largest entries first, never below 1
+    if (sum < target_total) {
+      u32 m = 0;
+      for (u32 i = 1; i < n_symbols; ++i)
+        if (c[i] > c[m]) m = i;
+      c[m] += target_total - sum;
+    } else if (sum > target_total) {
+      u64 excess = sum - target_total;
+      std::vector<u32> order(n_symbols);
+      for (u32 i = 0; i < n_symbols; ++i) order[i] = i;
+      std::stable_sort(order.begin(), order.end(), [&](u32 a, u32 b) { return c[a] > c[b]; });
+      for (u32 j = 0; j < n_symbols && excess; ++j) {
+        const u32 i = order[j];
+        if (c[i] <= 1) break;
+        const u64 take = std::min<u64>(excess, c[i] - 1);
+        c[i] -= take;
+        excess -= take;
+      }
+      if (excess) return RC_E_BAD_MODEL;  // unreachable: target >= number of entries
+    }
+  }
+  u64 acc = 0;
+  for (u32 i = 0; i < n_symbols; ++i) {
+    cum_out[i] = (u32)acc;
+    c_out[i] = (u32)c[i];
+    acc += c[i];
+    if (acc > 0xFFFFFFFFull) return RC_E_BAD_MODEL;  // calc_cum's u32 total would overflow
+  }
+  if (acc == 0) return RC_E_BAD_MODEL;
+  *total_out = (u32)acc;
+  return RC_OK;
+}
+
+rc_status rc_ideal_bits(rc_ctx* ctx, const uint32_t* c_host, uint32_t n_symbols,
+                        uint32_t total_freq, const uint32_t* chunk_hist, uint32_t n_chunks,
+                        double* bits) {
+  hipStream_t s;
+  int dev;
+  if (rc_ctx_stream_(ctx, &s, &dev) != RC_OK || !c_host || n_symbols < 1 || n_symbols > 256 ||
+      total_freq < 1 || n_chunks > RC_MAX_CHUNKS)
+    return RC_E_ARG;
+  if (n_chunks == 0) return RC_OK;
+  if (!chunk_hist || !bits) return RC_E_ARG;
+  // PModel::ideal_code_length (pmodel.rs:14-40): (ln total - ln c) / ln 2; symbols outside the
+  // alphabet or with c == 0 have no code length (+inf here)
+  double icl[256];
+  const double lt = log((double)total_freq);
+  for (u32 i = 0; i < 256; ++i)
+    icl[i] = (i < n_symbols && c_host[i] > 0) ? (lt - log((double)c_host[i])) / M_LN2 : INFINITY;
+  DevSet g(dev);
+  double* d = nullptr;
+  if (hipMallocAsync((void**)&d, sizeof icl, s) != hipSuccess) return RC_E_DEVICE;
+  if (hipMemcpyAsync(d, icl, sizeof icl, hipMemcpyHostToDevice, s) != hipSuccess) {
+    (void)hipFreeAsync(d, s);
+    return RC_E_DEVICE;
+  }
+  hipLaunchKernelGGL(k_ideal_bits, dim3((n_chunks + HWG - 1) / HWG), dim3(HWG), 0, s, d,
+                     chunk_hist, n_chunks, bits);
+  const bool ok = hipGetLastError() == hipSuccess;
+  // icl lives on the host stack: wait for the copy before returning
+  const bool fr = hipFreeAsync(d, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+  return ok && fr ? RC_OK : RC_E_DEVICE;
+}
+
+}  // extern "C"
