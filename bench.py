@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--no-adaptive", action="store_true", help="skip the adaptive (C4) leg")
     p.add_argument("--no-model-build", action="store_true",
                    help="skip the histogram / entropy-report leg (on the Zipf inputs)")
+    p.add_argument("--no-container", action="store_true",
+                   help="skip the container pack / unpack leg (on the Zipf code)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU sample wall time")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
@@ -182,6 +184,35 @@ def model_build_leg(torch, rc, leg, code_bytes, reps=3):
         built_table_total=total, built_table_max_c=int(c.max()), built_table_min_c=int(c.min()))
 
 
+def container_leg(torch, rc, leg):
+    """SURVEY.md §8f row 1 on the leg's encoded slots: rc_container_pack (scans + the payload
+    gather: reads the code, writes the container; HBM-bound) and rc_container_offsets (the
+    decode side's index scan), then a decode straight from the container, checked."""
+    t0, t1, t2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    blob = rc.container.pack(leg.model, leg.out, leg.out_off, leg.out_len, leg.sym_off)  # warm
+    del blob
+    torch.cuda.synchronize()
+    t0.record()
+    blob = rc.container.pack(leg.model, leg.out, leg.out_off, leg.out_len, leg.sym_off)
+    t1.record()
+    inf = rc.container.info(blob)
+    code_off, code_len, sym_off = rc.container.offsets(blob, inf)
+    t2.record()
+    torch.cuda.synchronize()
+    pack_ms = t0.elapsed_time(t1)
+    code = int(leg.out_len.sum())
+    moved = code + int(inf.container_bytes)
+    leg.dec.zero_()
+    fl = rc.decode_batch(leg.model, blob, code_off, code_len, leg.dec, sym_off)
+    ok = int(fl.abs().sum()) == 0 and equal_chunked(torch, leg.dec, leg.syms)
+    del blob
+    return dict(container_bytes=int(inf.container_bytes),
+                framing_overhead=round(int(inf.container_bytes) / code - 1, 6),
+                pack_ms=round(pack_ms, 3), pack_gbps=round(moved / pack_ms / 1e6, 1),
+                pack_roofline_frac=round(moved / pack_ms / 1e6 / HBM_PEAK_GBPS, 4),
+                offsets_ms=round(t1.elapsed_time(t2), 3), decode_from_container_ok=ok)
+
+
 def cpu_baseline(torch, leg, seconds, threads):
     """The C oracle (a bit-exact restatement of the Rust reference) on host cores, on a bounded
     sample of the same chunks (copied from HBM), encode + decode, Gsymbols/s round trip."""
@@ -287,6 +318,8 @@ def main():
             bit_exact_round_trip=zr["ok"])
         if not args.no_model_build:
             extras["model_build"] = model_build_leg(torch, rc, z, zr["code_bytes"])
+        if not args.no_container:
+            extras["container"] = container_leg(torch, rc, z)
     if not args.no_adaptive and args.config == "uniform" and L % 16384 == 0:
         La = 16384
         na = n * (L // La)

@@ -38,6 +38,8 @@ typedef int rc_status;
 #define RC_E_DEVICE (-3)    /* HIP runtime error (launch, allocation, copy) */
 #define RC_E_NO_DEVICE (-4) /* no gfx950 device visible / device index out of range */
 #define RC_E_CHUNK (-5)     /* synchronous helpers only: at least one chunk has a flag set */
+#define RC_E_BAD_CONTAINER (-6) /* container header / index malformed or inconsistent */
+#define RC_E_CAPACITY (-7)  /* destination buffer too small (the needed size is reported) */
 
 /* ---- per-chunk flags (bitwise; the first error of a chunk wins) ----
  * Where the reference panics or never terminates, the kernels flag the chunk instead.      */
@@ -168,6 +170,44 @@ rc_status rc_quantize_counts(const uint64_t* counts_host, uint32_t n_symbols,
 rc_status rc_ideal_bits(rc_ctx* ctx, const uint32_t* c_freq_host, uint32_t n_symbols,
                         uint32_t total_freq, const uint32_t* chunk_hist_dev, uint32_t n_chunks,
                         double* bits_dev);
+
+/* ---- chunked container "RCB1"  ----
+ * The reference's stream carries neither its symbol count (sample_impl.rs:113-120) nor its
+ * model (decoder.rs:38).  The container frames a batch of chunk streams with both:
+ *   offset 0          header, RC_CONTAINER_HEADER_BYTES, little-endian:
+ *                       0 "RCB1"  4 u32 version 1 | header bytes << 16  8 u32 kind (0 static,
+ *                       1 adaptive)  12 u32 n_symbols  16 u32 total_freq (static)
+ *                       20/24/28 u32 increment/limit/period (adaptive)  32 u64 n_chunks
+ *                       40 u64 symbols in all chunks  48 u64 payload bytes  56 reserved (0)
+ *   table_off = 64    static: n_symbols x u32 c_freq (cum rebuilt by calc_cum), zero padded
+ *                     to 16 B; adaptive: empty
+ *   index_off         n_chunks x {u64 symbol count, u64 code length}
+ *   payload_off       = index_off + 16 n_chunks; chunk k's code stream starts at payload_off +
+ *                     sum_{j<k} pad16(code length j), zero padded to 16 B
+ * A container is produced from encode_batch's slots and read back for decode_batch.        */
+#define RC_CONTAINER_HEADER_BYTES 64
+typedef struct rc_container_info {
+  uint32_t version, kind, n_symbols, total_freq, increment, limit, period, reserved;
+  uint64_t n_chunks, n_syms, payload_bytes;
+  uint64_t table_off, index_off, payload_off, container_bytes;
+} rc_container_info;
+
+/* Pack encoded slots (rc_encode_batch's out/out_off/out_len, chunk sizes from sym_off) and
+ * the model into a container at dst_dev.  Synchronous.  *dst_len_host receives the container
+ * size; RC_E_CAPACITY (nothing written) when it exceeds dst_cap or dst_dev is NULL.        */
+rc_status rc_container_pack(rc_ctx* ctx, const rc_model* m, const uint8_t* slots_dev,
+                            const uint64_t* slot_off_dev, const uint64_t* code_len_dev,
+                            const uint64_t* sym_off_dev, uint32_t n_chunks, uint8_t* dst_dev,
+                            uint64_t dst_cap, uint64_t* dst_len_host);
+/* Parse the header (head_host: the first >= RC_CONTAINER_HEADER_BYTES bytes). */
+rc_status rc_container_info_parse(const uint8_t* head_host, uint64_t head_len,
+                                  rc_container_info* info);
+/* Decode arguments from a device-resident container: code_off/code_len (n_chunks each, into
+ * the container), sym_off (n_chunks + 1).  Synchronous; RC_E_BAD_CONTAINER when the index does
+ * not add up to the header's payload and symbol totals.                                    */
+rc_status rc_container_offsets(rc_ctx* ctx, const uint8_t* container_dev,
+                               const rc_container_info* info, uint64_t* code_off_dev,
+                               uint64_t* code_len_dev, uint64_t* sym_off_dev);
 
 #ifdef __cplusplus
 }

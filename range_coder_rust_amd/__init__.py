@@ -8,5 +8,7 @@ from .api import (  # noqa: F401
 )
 from . import synth  # noqa: F401
 from .model_build import build_model, histogram, ideal_bits, quantize_counts  # noqa: F401
+from . import container  # noqa: F401
+from .container import ContainerError, compress, decompress  # noqa: F401
 
 __version__ = "0.1.0"

@@ -29,7 +29,19 @@ EXPORTS = (
     "rc_status_string", "rc_last_error", "rc_device_info", "rc_model_create_static",
     "rc_model_create_adaptive", "rc_model_destroy", "rc_encode_batch", "rc_decode_batch", "rc_encode_host",
     "rc_decode_host", "rc_synth_fill", "rc_histogram", "rc_quantize_counts", "rc_ideal_bits",
+    "rc_container_pack", "rc_container_info_parse", "rc_container_offsets",
 )
+RC_E_BAD_CONTAINER = -6
+RC_E_CAPACITY = -7
+CONTAINER_HEADER_BYTES = 64
+
+
+class ContainerInfo(ctypes.Structure):
+    """rc_container_info (include/range_coder.h)."""
+    _fields_ = [(n, ctypes.c_uint32) for n in ("version", "kind", "n_symbols", "total_freq",
+                                              "increment", "limit", "period", "reserved")] + \
+               [(n, ctypes.c_uint64) for n in ("n_chunks", "n_syms", "payload_bytes", "table_off",
+                                              "index_off", "payload_off", "container_bytes")]
 Q_ALL_SYMBOLS = 1
 
 _P = ctypes.c_void_p
@@ -78,6 +90,9 @@ def load():
     L.rc_histogram.argtypes = [_P, _P, _P, _U32, _P, _P]
     L.rc_quantize_counts.argtypes = [_P, _U32, _U64, _U32, _P, _P, _P]
     L.rc_ideal_bits.argtypes = [_P, _P, _U32, _U32, _P, _U32, _P]
+    L.rc_container_pack.argtypes = [_P, _P, _P, _P, _P, _P, _U32, _P, _U64, ctypes.POINTER(_U64)]
+    L.rc_container_info_parse.argtypes = [_P, _U64, ctypes.POINTER(ContainerInfo)]
+    L.rc_container_offsets.argtypes = [_P, _P, ctypes.POINTER(ContainerInfo), _P, _P, _P]
     for name in EXPORTS:
         if name not in ("rc_status_string", "rc_last_error"):
             getattr(L, name).restype = _I

@@ -17,6 +17,7 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 // instruction stream allocated 96 VGPRs is correct.  Each kernel clobbers a
 // register so its allocation is a multiple of 16; build() rejects any other count.
 #define RC_VGPR_FLOOR_32() asm volatile("; vgpr floor 32" ::: "v31")
+#define RC_VGPR_FLOOR_48() asm volatile("; vgpr floor 48" ::: "v47")
 #define RC_VGPR_FLOOR_64() asm volatile("; vgpr floor 64" ::: "v63")
 #define RC_VGPR_FLOOR_96() asm volatile("; vgpr floor 96" ::: "v95")
 #define RC_VGPR_FLOOR_112() asm volatile("; vgpr floor 112" ::: "v111")

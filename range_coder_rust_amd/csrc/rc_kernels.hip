@@ -798,7 +798,9 @@ struct rc_model {
   int div;
   ModelArgs args;
   void* dmem;
-  AdaptParams ap;  // kind 1
+  AdaptParams ap;      // kind 1
+  u32 c_host[256];     // kind 0: the c_freq snapshot (container tables, entropy reports)
+  u32 period;          // kind 1: as given
 };
 
 namespace {
@@ -844,6 +846,8 @@ const char* rc_status_string(rc_status s) {
     case RC_E_DEVICE: return "HIP runtime error";
     case RC_E_NO_DEVICE: return "no usable gfx950 device";
     case RC_E_CHUNK: return "at least one chunk flagged";
+    case RC_E_BAD_CONTAINER: return "malformed container";
+    case RC_E_CAPACITY: return "destination too small";
     default: return "unknown status";
   }
 }
@@ -902,6 +906,22 @@ rc_status rc_ctx_stream_(rc_ctx* ctx, hipStream_t* s, int* device) {
   if (!ctx || !s || !device) return RC_E_ARG;
   *s = ctx->cur;
   *device = ctx->device;
+  return RC_OK;
+}
+
+// internal: what the container writer needs to know about a model
+rc_status rc_model_describe_(const rc_model* m, int* kind, int* device, uint32_t* n_symbols,
+                             uint32_t* total, const uint32_t** c_host, uint32_t* increment,
+                             uint32_t* limit, uint32_t* period) {
+  if (!m) return RC_E_ARG;
+  *kind = m->kind;
+  *device = m->device;
+  *n_symbols = m->kind == 0 ? m->args.n : m->ap.n;
+  *total = m->args.total;
+  *c_host = m->c_host;
+  *increment = m->ap.inc;
+  *limit = m->ap.limit;
+  *period = m->period;
   return RC_OK;
 }
 
@@ -1009,6 +1029,9 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
   mm->args = a;
   mm->dmem = d;
   mm->ap = AdaptParams{};
+  memset(mm->c_host, 0, sizeof mm->c_host);
+  for (u32 i = 0; i < n_symbols; ++i) mm->c_host[i] = c_freq[i];
+  mm->period = 0;
   *out = mm;
   return RC_OK;
 }
@@ -1026,6 +1049,7 @@ rc_status rc_model_create_adaptive(rc_ctx* ctx, uint32_t n_symbols, uint32_t inc
   mm->kind = 1;
   mm->device = ctx->device;
   mm->ap = AdaptParams{n_symbols, increment, limit, period - 1};
+  mm->period = period;
   *out = mm;
   return RC_OK;
 }
