@@ -49,6 +49,8 @@ def parse():
                    help="skip the histogram / entropy-report leg (on the Zipf inputs)")
     p.add_argument("--no-container", action="store_true",
                    help="skip the container pack / unpack leg (on the Zipf code)")
+    p.add_argument("--no-host-stream", action="store_true",
+                   help="skip the host-resident (PCIe) encode/decode leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU sample wall time")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
@@ -213,6 +215,58 @@ def container_leg(torch, rc, leg):
                 offsets_ms=round(t1.elapsed_time(t2), 3), decode_from_container_ok=ok)
 
 
+def host_stream_leg(torch, rc, leg, n_chunks):
+    """host-resident chunks through rc_encode_host / rc_decode_host
+    (pipelined H2D / kernel / D2H over 3 streams).  "pinned": every host buffer is pinned
+    memory (torch pin_memory) — the pipeline's own rate; "pageable": fresh numpy buffers, which
+    the call page-locks in place (first-touch + pinning cost included).  Rates are symbol bytes
+    per second end to end (PCIe-inclusive); never the headline value."""
+    L = leg.L
+    n = min(n_chunks, leg.n)
+    soff = np.arange(n + 1, dtype=np.uint64) * L
+    ooff = np.arange(n + 1, dtype=np.uint64) * leg.cap
+    res = {}
+    for kind in ("pinned", "pageable"):
+        if kind == "pinned":
+            hs = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+            hs.copy_(leg.syms[: n * L])
+            syms = hs.numpy()
+            out = torch.empty(n * leg.cap, dtype=torch.uint8, pin_memory=True).numpy()
+            dec = torch.empty(n * L, dtype=torch.uint8, pin_memory=True).numpy()
+        else:
+            syms = leg.syms[: n * L].cpu().numpy()
+            out = dec = None
+        times = []
+        for rep in range(2 if kind == "pinned" else 1):
+            t0 = time.perf_counter()
+            out, ol, fl = rc.encode_host(leg.model, syms, soff, ooff, out=out)
+            t1 = time.perf_counter()
+            dec, fd = rc.decode_host(leg.model, out, ooff[:-1], ol, soff, out=dec)
+            t2 = time.perf_counter()
+            times.append((t1 - t0, t2 - t1))
+        te, td = times[-1]
+        ok = bool((fl == 0).all() and (fd == 0).all() and np.array_equal(dec, syms))
+        res[kind] = dict(encode_gbps=round(n * L / te / 1e9, 2),
+                         decode_gbps=round(n * L / td / 1e9, 2), round_trip_ok=ok)
+        del out, dec, syms
+    res["sample"] = f"{n} x {L // 1024} KiB chunks ({n * L / 2**30:.1f} GiB) host-resident"
+    # the bound of this leg: plain pinned copies of 1 GiB each way on this box
+    hb = torch.empty(1 << 30, dtype=torch.uint8, pin_memory=True)
+    db = torch.empty(1 << 30, dtype=torch.uint8, device=leg.syms.device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    db.copy_(hb, non_blocking=True)
+    ev[0].record()
+    db.copy_(hb, non_blocking=True)
+    ev[1].record()
+    hb.copy_(db, non_blocking=True)
+    ev[2].record()
+    torch.cuda.synchronize()
+    res["pcie_h2d_gbps"] = round((1 << 30) / ev[0].elapsed_time(ev[1]) / 1e6, 2)
+    res["pcie_d2h_gbps"] = round((1 << 30) / ev[1].elapsed_time(ev[2]) / 1e6, 2)
+    del hb, db
+    return res
+
+
 def cpu_baseline(torch, leg, seconds, threads):
     """The C oracle (a bit-exact restatement of the Rust reference) on host cores, on a bounded
     sample of the same chunks (copied from HBM), encode + decode, Gsymbols/s round trip."""
@@ -320,6 +374,8 @@ def main():
             extras["model_build"] = model_build_leg(torch, rc, z, zr["code_bytes"])
         if not args.no_container:
             extras["container"] = container_leg(torch, rc, z)
+        if not args.no_host_stream and world == 1:
+            extras["host_stream"] = host_stream_leg(torch, rc, z, 131072)
     if not args.no_adaptive and args.config == "uniform" and L % 16384 == 0:
         La = 16384
         na = n * (L // La)

@@ -4,7 +4,7 @@ from .api import (  # noqa: F401
     ADAPTIVE_DEFAULTS, AdaptiveModel, BadSymbolError, CapacityError, Context, CorruptStreamError, Decoder, Encoder, FreqTable,
     PModel, RangeCoderError, StaticModel, TruncatedStreamError, ZeroFrequencyError,
     decode_batch, decode_chunks, default_context, encode_batch, encode_chunks, flag_names,
-    slot_capacity,
+    slot_capacity, encode_host, decode_host,
 )
 from . import synth  # noqa: F401
 from .model_build import build_model, histogram, ideal_bits, quantize_counts  # noqa: F401

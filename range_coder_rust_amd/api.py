@@ -509,3 +509,55 @@ def _snapshot(pmodel):
     m = StaticModel(sig[0], sig[1], sig[2])
     _snap_cache[key] = (sig, m)
     return m
+
+
+# ----------------------------------------------------------------------------- host streaming
+def _np_ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a.size else ctypes.c_void_p(0)
+
+
+def encode_host(model, syms, sym_off, out_off, out=None):
+    """rc_encode_host: host-resident numpy arrays through the pipelined H2D / encode / D2H
+    stream (rc_stream.hip).  Returns (out uint8[out_off[-1]], out_len uint64[n], flags
+    uint32[n]); flags are returned, not raised.  out: optional caller buffer (e.g. a view of
+    pinned memory, which skips the per-call page locking)."""
+    syms = np.ascontiguousarray(syms, dtype=np.uint8)
+    sym_off = np.ascontiguousarray(sym_off, dtype=np.uint64)
+    out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
+    n = len(sym_off) - 1
+    if out is None:
+        out = np.empty(int(out_off[-1]), np.uint8)
+    elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < int(out_off[-1]):
+        raise ValueError("out must be a contiguous uint8 array of out_off[-1] bytes")
+    out_len = np.zeros(max(n, 1), np.uint64)
+    flags = np.zeros(max(n, 1), np.uint32)
+    ctx = model.ctx
+    rc = ctx._lib.rc_encode_host(ctx.handle, model.handle, _np_ptr(syms), _np_ptr(sym_off), n,
+                                 _np_ptr(out), _np_ptr(out_off), _np_ptr(out_len), _np_ptr(flags))
+    if rc not in (N.RC_OK, N.RC_E_CHUNK):
+        N.check(rc, "rc_encode_host")
+    return out, out_len[:n], flags[:n]
+
+
+def decode_host(model, code, code_off, code_len, sym_off, out=None):
+    """rc_decode_host: the pipelined host path of decode_batch.  Returns (syms, flags).
+    out: optional caller buffer for the symbols."""
+    code = np.ascontiguousarray(code, dtype=np.uint8)
+    code_off = np.ascontiguousarray(code_off, dtype=np.uint64)
+    code_len = np.ascontiguousarray(code_len, dtype=np.uint64)
+    sym_off = np.ascontiguousarray(sym_off, dtype=np.uint64)
+    n = len(sym_off) - 1
+    if out is None:
+        syms = np.empty(int(sym_off[-1]), np.uint8)
+    elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < int(sym_off[-1]):
+        raise ValueError("out must be a contiguous uint8 array of sym_off[-1] bytes")
+    else:
+        syms = out
+    flags = np.zeros(max(n, 1), np.uint32)
+    ctx = model.ctx
+    rc = ctx._lib.rc_decode_host(ctx.handle, model.handle, _np_ptr(code), _np_ptr(code_off),
+                                 _np_ptr(code_len), _np_ptr(syms), _np_ptr(sym_off), n,
+                                 _np_ptr(flags))
+    if rc not in (N.RC_OK, N.RC_E_CHUNK):
+        N.check(rc, "rc_decode_host")
+    return syms, flags[:n]

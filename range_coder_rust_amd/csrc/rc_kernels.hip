@@ -1132,87 +1132,7 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   return launch_status();
 }
 
-namespace {
-// Synchronous staging through device memory for the host-pointer helpers.
-struct DevBuf {
-  void* p = nullptr;
-  hipStream_t s;
-  explicit DevBuf(hipStream_t st) : s(st) {}
-  bool alloc(size_t n) { return hipMalloc(&p, n ? n : 16) == hipSuccess; }
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-};
-
-rc_status any_flag(const uint32_t* flags, uint32_t n) {
-  for (uint32_t i = 0; i < n; ++i)
-    if (flags[i]) return RC_E_CHUNK;
-  return RC_OK;
-}
-}  // namespace
-
-rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
-                         const uint64_t* sym_off, uint32_t n_chunks, uint8_t* out,
-                         const uint64_t* out_off, uint64_t* out_len, uint32_t* flags) {
-  if (!ctx || !m || n_chunks > RC_MAX_CHUNKS) return RC_E_ARG;
-  if (n_chunks == 0) return RC_OK;
-  if (!syms || !sym_off || !out || !out_off || !out_len || !flags) return RC_E_ARG;
-  DeviceGuard g(ctx->device);
-  if (!g.ok) return RC_E_DEVICE;
-  const size_t nsym = sym_off[n_chunks], nout = out_off[n_chunks], noff = 8 * (n_chunks + 1);
-  hipStream_t s = ctx->cur;
-  DevBuf dsyms(s), dsoff(s), dout(s), doo(s), dlen(s), dfl(s);
-  if (!dsyms.alloc(nsym) || !dsoff.alloc(noff) || !dout.alloc(nout) || !doo.alloc(noff) ||
-      !dlen.alloc(8 * n_chunks) || !dfl.alloc(4 * n_chunks))
-    return RC_E_DEVICE;
-  if (hipMemcpyAsync(dsyms.p, syms, nsym, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(dsoff.p, sym_off, noff, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(doo.p, out_off, noff, hipMemcpyHostToDevice, s) != hipSuccess)
-    return RC_E_DEVICE;
-  rc_status st = rc_encode_batch(ctx, m, (const uint8_t*)dsyms.p, (const uint64_t*)dsoff.p,
-                                 n_chunks, (uint8_t*)dout.p, (const uint64_t*)doo.p,
-                                 (uint64_t*)dlen.p, (uint32_t*)dfl.p);
-  if (st != RC_OK) return st;
-  if (hipMemcpyAsync(out, dout.p, nout, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(out_len, dlen.p, 8 * n_chunks, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(flags, dfl.p, 4 * n_chunks, hipMemcpyDeviceToHost, s) != hipSuccess)
-    return RC_E_DEVICE;
-  if (hipStreamSynchronize(s) != hipSuccess) return RC_E_DEVICE;
-  return any_flag(flags, n_chunks);
-}
-
-rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
-                         const uint64_t* code_off, const uint64_t* code_len, uint8_t* syms_out,
-                         const uint64_t* sym_off, uint32_t n_chunks, uint32_t* flags) {
-  if (!ctx || !m || n_chunks > RC_MAX_CHUNKS) return RC_E_ARG;
-  if (n_chunks == 0) return RC_OK;
-  if (!code || !code_off || !code_len || !syms_out || !sym_off || !flags) return RC_E_ARG;
-  DeviceGuard g(ctx->device);
-  if (!g.ok) return RC_E_DEVICE;
-  size_t ncode = 0;
-  for (uint32_t i = 0; i < n_chunks; ++i)
-    ncode = std::max<size_t>(ncode, (size_t)(code_off[i] + code_len[i]));
-  const size_t nsym = sym_off[n_chunks], noff = 8 * (n_chunks + 1);
-  hipStream_t s = ctx->cur;
-  DevBuf dcode(s), dcoff(s), dclen(s), dsyms(s), dsoff(s), dfl(s);
-  if (!dcode.alloc(ncode + 16) || !dcoff.alloc(8 * n_chunks) || !dclen.alloc(8 * n_chunks) ||
-      !dsyms.alloc(nsym) || !dsoff.alloc(noff) || !dfl.alloc(4 * n_chunks))
-    return RC_E_DEVICE;
-  if (hipMemcpyAsync(dcode.p, code, ncode, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(dcoff.p, code_off, 8 * n_chunks, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(dclen.p, code_len, 8 * n_chunks, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(dsoff.p, sym_off, noff, hipMemcpyHostToDevice, s) != hipSuccess)
-    return RC_E_DEVICE;
-  rc_status st = rc_decode_batch(ctx, m, (const uint8_t*)dcode.p, (const uint64_t*)dcoff.p,
-                                 (const uint64_t*)dclen.p, (uint8_t*)dsyms.p,
-                                 (const uint64_t*)dsoff.p, n_chunks, (uint32_t*)dfl.p);
-  if (st != RC_OK) return st;
-  if (hipMemcpyAsync(syms_out, dsyms.p, nsym, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(flags, dfl.p, 4 * n_chunks, hipMemcpyDeviceToHost, s) != hipSuccess)
-    return RC_E_DEVICE;
-  if (hipStreamSynchronize(s) != hipSuccess) return RC_E_DEVICE;
-  return any_flag(flags, n_chunks);
-}
+// rc_encode_host / rc_decode_host: the pipelined host path lives in rc_stream.hip
 
 rc_status rc_synth_fill(rc_ctx* ctx, uint64_t seed, const uint8_t* inv_cdf_host,
                         uint8_t* syms_dev, uint64_t chunk_len, uint32_t n_chunks) {

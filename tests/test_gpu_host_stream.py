@@ -1,0 +1,106 @@
+"""GPU parity of the pipelined host path (rc_stream.hip): rc_encode_host /
+rc_decode_host on host-resident numpy arrays against the oracle, byte for byte, across many
+small batches (RC_STREAM_BATCH_BYTES lowered), ragged / misaligned / scattered layouts, flagged
+chunks, and pageable vs pinned buffers."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import range_coder_rust_amd as rc  # noqa: E402
+from range_coder_rust_amd import synth  # noqa: E402
+from oracle import cpu  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return rc.default_context(0)
+
+
+@pytest.fixture
+def small_batches(monkeypatch):
+    monkeypatch.setenv("RC_STREAM_BATCH_BYTES", "20000")
+
+
+def layout(rng, n, lo, hi, gap=False):
+    lens = rng.integers(lo, hi + 1, n)
+    lens[rng.random(n) < 0.1] = 0
+    gaps = rng.integers(0, 40, n) if gap else np.zeros(n, np.int64)
+    off = np.zeros(n + 1, np.int64)
+    off[0] = int(rng.integers(0, 16)) if gap else 0
+    for k in range(n):
+        off[k + 1] = off[k] + lens[k] + (gaps[k] if k + 1 < n else 0)
+    return lens, off
+
+
+@pytest.mark.parametrize("gap", [False, True])
+def test_encode_host_matches_oracle(ctx, small_batches, gap):
+    rng = np.random.default_rng(3 + gap)
+    c, cum, total = synth.zipf_table()
+    m = rc.StaticModel(c, cum, total)
+    n = 120
+    lens, soff = layout(rng, n, 0, 3000, gap)
+    syms = rng.choice(256, int(soff[-1]), p=np.asarray(c, float) / np.sum(c)).astype(np.uint8)
+    caps = np.array([rc.slot_capacity(int(L), m.max_bits_per_symbol()) for L in lens])
+    ooff = np.concatenate([[int(rng.integers(0, 16)) if gap else 0], caps]).cumsum()
+    # chunk k's symbols are [soff[k], soff[k] + lens[k]); with gaps the offsets array has
+    # the gap bytes inside chunk k, so encode exactly what the offsets describe
+    out, ol, fl = rc.encode_host(m, syms, soff, ooff)
+    assert (fl == 0).all()
+    for k in range(n):
+        ch = syms[soff[k]: soff[k + 1]]
+        f, b, L = cpu.encode(c, cum, total, ch)
+        assert f == 0 and ol[k] == L and bytes(out[ooff[k]: ooff[k] + L]) == b, k
+    # decode from scattered code positions
+    counts = np.diff(soff)
+    dsoff = np.concatenate([[0], np.cumsum(counts)])
+    dec, fd = rc.decode_host(m, out, ooff[:-1], ol, dsoff)
+    assert (fd == 0).all()
+    assert (dec == syms[soff[0]: soff[-1]]).all()
+
+
+def test_flags_returned(ctx, small_batches):
+    m = rc.StaticModel([1, 5, 2, 0, 2, 2, 1, 1, 1, 1])
+    syms = np.array([1, 2, 3, 1, 2, 12], np.uint8)
+    soff = np.array([0, 3, 5, 6])
+    ooff = np.array([0, 64, 128, 192])
+    out, ol, fl = rc.encode_host(m, syms, soff, ooff)
+    assert list(fl) == [rc._native.F_ZERO_FREQ, 0, rc._native.F_BAD_SYMBOL]
+    f, b, L = cpu.encode([1, 5, 2, 0, 2, 2, 1, 1, 1, 1], [0, 1, 6, 8, 8, 10, 12, 13, 14, 15],
+                         16, bytes([1, 2]))
+    assert ol[1] == L and bytes(out[64:64 + L]) == b
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_large_round_trip(ctx, pinned):
+    n, L = 1200, 65536  # 75 MiB: two batches at the default batch size
+    dsyms = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    c, cum, total = synth.zipf_table()
+    synth.fill(ctx, 21, synth.inverse_cdf(c), dsyms, L, n)
+    if pinned:
+        hs = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+        hs.copy_(dsyms)
+        syms = hs.numpy()
+    else:
+        syms = dsyms.cpu().numpy()
+    m = rc.StaticModel(c, cum, total)
+    soff = np.arange(n + 1) * L
+    cap = rc.slot_capacity(L, 8.0)
+    ooff = np.arange(n + 1) * cap
+    out, ol, fl = rc.encode_host(m, syms, soff, ooff)
+    ol = ol.astype(np.int64)
+    assert (fl == 0).all()
+    # same bytes as the device path
+    dout = torch.empty(n * cap, dtype=torch.uint8, device="cuda")
+    dl, df = rc.encode_batch(m, dsyms, torch.from_numpy(soff).cuda(), dout,
+                             torch.from_numpy(ooff).cuda())
+    assert (dl.cpu().numpy() == ol.astype(np.int64)).all()
+    hd = dout.cpu().numpy()
+    for k in (0, 1, n // 2, n - 1):
+        assert bytes(hd[ooff[k]: ooff[k] + ol[k]]) == bytes(out[ooff[k]: ooff[k] + ol[k]])
+    dec, fd = rc.decode_host(m, out, ooff[:-1], ol, soff)
+    assert (fd == 0).all() and (dec == syms).all()
