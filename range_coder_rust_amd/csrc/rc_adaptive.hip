@@ -9,23 +9,38 @@
 // bit-exactly, as the static kernels do (the same closed-form renormalisation).
 //
 // Layout: one chunk per lane, one wave per workgroup.  Each lane's counts live in LDS as a
-// 255-node tree of u16 (32 KiB per wave).  Node 256 — the total — lives in a register.  The
-// tree is interleaved by lane, so one node row is one conflict-free 128-B access:
-//     node j (1..255) = the counts of symbols [j - lowbit(j), j).
-// Read top-down, that is the left-subtree-sum tree over the 256 symbols:
-//   * the encoder's (cum[s], c[s]) is a root-to-leaf walk of 8 independent loads;
-//   * the decoder's FreqTable::find_index (sample_impl.rs:27-45) is the same walk, steered by
-//     the target frequency (8 dependent loads); it also yields cum[s] and c[s];
-//   * c[s] += inc adds inc to the nodes where the walk went left (packed ds_add_u32).
-// Read as a Fenwick tree, it turns into counts and back in place for the halving.
+// 255-node tree of u16 (32 KiB per wave, so 5 waves per CU).  Node 256 — the total — lives in a
+// register.  The tree is interleaved by lane, so one node row is one conflict-free 128-B access:
+//     node j (1..255) = the counts of symbols [j - lowbit(j), j),  at byte (j-1)*128 + 2*lane.
+// Read top-down, that is the left-subtree-sum tree over the 256 symbols.  For symbol s, level l
+// (0..7) visits node (s & ~(2*step-1)) | step, step = 128 >> l, and turns right iff bit 7-l of s
+// is set.  Read as a Fenwick tree, it turns into counts and back in place for the halving.
 // Node values stay below 2^16 because the total does: limit + inc * period <= 65535.
-// range / total (range_coder.rs:38-40) uses a float64 reciprocal and an exact integer
-// correction.  Symbols and code move through per-lane dword loads and stores; L2 merges each
-// lane's partial lines.
+//
+// Encoder symbol step: the 8 path nodes are read one symbol ahead, packed in
+// u16 pairs, so cum[s] = sum over right turns and cum[s+1] = the same sum with the bits of s+1
+// (the walk of s+1 agrees with that of s above its lowest zero bit) are 4 v_dot2_u32_u16 each,
+// c[s] = cum[s+1] - cum[s], and the update c[s] += inc is 4 v_pk_mad_u16 written back as u16s.
+// Output bytes go through a 128-bit shift register; every 4 symbols its complete dwords are
+// stored as one 12-B write that also rewrites the (identical) dwords before them.
+//
+// Decoder symbol step: the target frequency comes from a float hint x * total / range; the top
+// three tree levels (7 nodes, fixed addresses) are read one symbol ahead, levels 3-5 are one
+// 7-node lookahead read and levels 6-7 one 3-node read, so the walk costs two dependent LDS
+// round trips.  The exact interval test r*cum <= x < r*(cum+c) then confirms the symbol
+// (FreqTable::find_index, sample_impl.rs:27-45); a wrong hint takes a rare exact path.
+//
+// range / total (range_coder.rs:38-40) uses a float64 reciprocal of the total (computed one
+// symbol ahead) and an exact integer correction.
 #include "rc_common.h"
 
-#define AWG 64                  // one wave per workgroup
-#define TREE_BYTES (255 * 64 * 2)
+#define AWG 64  // one wave per workgroup
+#define TREE_BYTES (255 * 128)
+#define ROW(j) (((j) - 1) * 128)  // byte offset of node j's row
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+static __device__ __forceinline__ u32 clz32(u32 v) { return (u32)__builtin_clz(v); }  // v != 0
 
 // ~1/t to well under 2^-40 relative error: v_rcp_f64 plus one Newton step
 static __device__ __forceinline__ double recip(u32 t) {
@@ -35,20 +50,50 @@ static __device__ __forceinline__ double recip(u32 t) {
 }
 
 // range_par_total (range_coder.rs:38-40): floor(v / t) for 1 <= t < 2^16, exact.  Each
-// quotient half is floor or floor - 1 from the float64 product, then corrected.
+// quotient half is floor or floor - 1 from the float64 product, then corrected.  The
+// corrections use sign masks (d >> 31), not compares: a VALU read of VCC (v_cndmask_b32_e32,
+// v_addc_co_u32) costs ~4x a plain op on gfx950 (tools/ubench_sel.hip).
+static __device__ __forceinline__ u32 fixup(u32& q, u32 rem, u32 t) {  // rem < 2t
+  const u32 d = rem - t;
+  q += 1u + (u32)((int)d >> 31);  // +1 unless rem < t
+  return min(rem, d);             // rem mod t
+}
 static __device__ __forceinline__ u64 div_total(u64 v, u32 t, double rt) {
   const u32 hi = hi32(v), lo = (u32)v;
   u32 qh = (u32)((double)hi * rt);
-  u32 rh = hi - qh * t;
-  const bool fh = rh >= t;
-  qh += fh ? 1u : 0u;
-  rh -= fh ? t : 0u;
+  const u32 rh = fixup(qh, hi - qh * t, t);
   const double num = fma((double)rh, 4294967296.0, (double)lo);  // < 2^48: exact
   u32 ql = (u32)(num * rt);
-  const u64 rl = (((u64)rh << 32) | lo) - (u64)ql * t;
-  ql += rl >= t ? 1u : 0u;
-  return ((u64)qh << 32) + ql;
+  fixup(ql, lo - ql * t, t);  // (rh:lo) - ql*t < 2t: its low 32 bits are the value
+  return ((u64)qh << 32) | ql;
 }
+
+// a - b (64-bit) with the borrow in an SGPR pair rather than VCC
+static __device__ __forceinline__ u64 sub64(u64 a, u64 b) {
+  u32 lo, hi;
+  u64 c;
+  asm("v_sub_co_u32_e64 %0, %2, %3, %4\n\tv_subb_co_u32_e64 %1, %2, %5, %6, %2"
+      : "=&v"(lo), "=&v"(hi), "=&s"(c)
+      : "v"((u32)a), "v"((u32)b), "v"(hi32(a)), "v"(hi32(b)));
+  return ((u64)hi << 32) | lo;
+}
+
+// (m & a) | (~m & b) for a mask m of 0 / ~0: one v_bfi_b32.  The empty asm hides that m is a
+// mask, or the compiler turns this back into v_cmp + v_cndmask_b32 on VCC.
+static __device__ __forceinline__ u32 msel(u32 m, u32 a, u32 b) {
+  asm("" : "+v"(m));
+  return (m & a) | (~m & b);
+}
+
+// r * v for v < 2^16 (r < 2^64 / v: no overflow)
+static __device__ __forceinline__ u64 mul_r(u64 r, u32 v) {
+  return (u64)(u32)r * v + ((u64)(hi32(r) * v) << 32);
+}
+
+// ---- LDS access by byte address (this kernel's only LDS is the dynamic tree, at offset 0) ----
+typedef __attribute__((address_space(3))) uint16_t l_u16;
+static __device__ __forceinline__ u32 lrd(u32 a) { return *(const l_u16*)(uintptr_t)a; }
+static __device__ __forceinline__ void lwr(u32 a, u32 v) { *(l_u16*)(uintptr_t)a = (uint16_t)v; }
 
 // ---- the per-lane count tree: node j at t[(j - 1) * 64] ----
 
@@ -59,57 +104,8 @@ static __device__ __forceinline__ void tree_init(uint16_t* t, u32 n) {
   }
 }
 
-// cum[s] and c[s]: the walk to leaf s goes right at level l iff bit 7-l of s is set
-static __device__ __forceinline__ void tree_query(const uint16_t* t, u32 s, u32 total, u32& cum,
-                                                  u32& c) {
-  u32 v[8];
-#pragma unroll
-  for (int l = 0; l < 8; ++l) {
-    const u32 step = 128u >> l;
-    v[l] = t[(((s & ~(2 * step - 1)) | step) - 1) * 64];
-  }
-  u32 a = 0, b = total;
-#pragma unroll
-  for (int l = 0; l < 8; ++l) {
-    const bool right = (s & (128u >> l)) != 0;
-    a += right ? v[l] : 0u;
-    b = right ? b - v[l] : v[l];
-  }
-  cum = a;
-  c = b;
-}
-
-// FreqTable::find_index for q < total: the s with cum[s] <= q < cum[s] + c[s]
-static __device__ __forceinline__ u32 tree_find(const uint16_t* t, u32 q, u32 total, u32& cum,
-                                                u32& c) {
-  u32 pos = 0, rem = q, b = total;
-#pragma unroll
-  for (int l = 0; l < 8; ++l) {
-    const u32 j = pos | (128u >> l);
-    const u32 v = t[(j - 1) * 64];
-    const bool right = rem >= v;
-    pos = right ? j : pos;
-    rem = right ? rem - v : rem;
-    b = right ? b - v : v;
-  }
-  cum = q - rem;
-  c = b;
-  return pos;
-}
-
-// c[s] += inc: every node whose left subtree holds s.  tw: this lane's dword column (the
-// lane pair's u16s share a dword; incv = inc in this lane's half, no carry: nodes < 2^16)
-static __device__ __forceinline__ void tree_add(u32* tw, u32 s, u32 incv) {
-#pragma unroll
-  for (int l = 0; l < 8; ++l) {
-    const u32 step = 128u >> l;
-    // unconditional (adding 0 where the walk went right): no exec-mask branch per level
-    atomicAdd(&tw[(((s & ~(2 * step - 1)) | step) - 1) * 32], (s & step) ? 0u : incv);
-  }
-}
-
 // every c = (c + 1) >> 1: Fenwick -> counts (reverse pass), halve, counts -> Fenwick
-static __device__ void tree_halve(uint16_t* t, u32& total) {
+static __device__ __forceinline__ void tree_halve(uint16_t* t, u32& total) {
   for (u32 j = 255; j >= 1; --j) {
     const u32 k = j + (j & (0u - j));
     if (k < 256) t[(k - 1) * 64] = (uint16_t)(t[(k - 1) * 64] - t[(j - 1) * 64]);
@@ -129,228 +125,444 @@ static __device__ void tree_halve(uint16_t* t, u32& total) {
   total = nt;
 }
 
-// ------------------------------------------------------------------------------------------
-// I/O.  Memory traffic happens only at phase boundaries (every 16 symbols, at the same symbol
-// index in every lane): first the block loaded one boundary earlier is consumed (the only
-// wait), then this phase's stores are issued, then the next load.  So no wait ever covers a
-// recent memory operation.  A conditional per-lane prefetch does not achieve this: the value
-// merge at the branch join makes the compiler wait for the load right after issuing it.
-// ------------------------------------------------------------------------------------------
+// FreqTable::find_index for q < total (rare exact path): the s with cum[s] <= q < cum[s]+c[s]
+static __device__ __forceinline__ u32 tree_find(const uint16_t* t, u32 q, u32 total, u32& cum, u32& c) {
+  u32 pos = 0, rem = q, b = total;
+  for (int l = 0; l < 8; ++l) {
+    const u32 j = pos | (128u >> l);
+    const u32 v = t[(j - 1) * 64];
+    const bool right = rem >= v;
+    pos = right ? j : pos;
+    rem = right ? rem - v : rem;
+    b = right ? b - v : v;
+  }
+  cum = q - rem;
+  c = b;
+  return pos;
+}
+
+// c[s] += inc (rare exact path): every node whose left subtree holds s
+static __device__ __forceinline__ void tree_add(uint16_t* t, u32 s, u32 inc) {
+  for (int l = 0; l < 8; ++l) {
+    const u32 step = 128u >> l;
+    if (!(s & step)) {
+      uint16_t* p = t + ((((s & ~(2 * step - 1)) | step) - 1) * 64);
+      *p = (uint16_t)(*p + inc);
+    }
+  }
+}
+
+static __device__ __forceinline__ u32 wave_min(u32 v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, (u32)__shfl_xor((int)v, o));
+  return v;
+}
+static __device__ __forceinline__ u32 wave_max(u32 v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, (u32)__shfl_xor((int)v, o));
+  return v;
+}
+
+// byte j (0..15, per lane) of a 16-B block in registers
+static __device__ __forceinline__ u32 byte_at(const u32x4& b, u32 j) {
+  u32 w = b.x;
+  w = (j >> 2) == 1 ? b.y : w;
+  w = (j >> 2) == 2 ? b.z : w;
+  w = (j >> 2) == 3 ? b.w : w;
+  return (w >> (8 * (j & 3))) & 255u;
+}
 
 __device__ u32x4 g_zero16;  // load target of lanes without input (never written)
-
-
-// 4 bytes at byte offset (dsh * 4 + bsh) of the 8-dword window v: v[dsh], v[dsh + 1] funnel
-static __device__ __forceinline__ u32 pick4(const u32 (&v)[8], u32 k, u32 dsh, u32 bsh) {
-  // v[dsh + k] and v[dsh + k + 1] for a per-lane dsh in 0..3
-  u32 a = v[k], b = v[k + 1];
-  a = dsh == 1 ? v[k + 1] : a;
-  b = dsh == 1 ? v[k + 2] : b;
-  a = dsh == 2 ? v[k + 2] : a;
-  b = dsh == 2 ? v[k + 3] : b;
-  a = dsh == 3 ? v[k + 3] : a;
-  b = dsh == 3 ? v[k + 4] : b;
-  return __builtin_amdgcn_alignbyte(b, a, bsh);
-}
 
 // ------------------------------------------------------------------------------------------
 // Encoder
 // ------------------------------------------------------------------------------------------
 
-// A settled dword (stream order, first byte in the top bits) at dp, clipped to [lo, hi).  dp
-// is 4-B aligned because the stream starts with (slot address & 3) phantom bytes.
-static __device__ __forceinline__ void put_dword(uint8_t*& dp, u32 be, const uint8_t* lo,
-                                                 const uint8_t* hi) {
-  const u32 d = __builtin_bswap32(be);
-  if (dp >= lo && dp + 4 <= hi) {
-    gstore32(dp, d);
-  } else {
-    for (u32 j = 0; j < 4; ++j)
-      if (dp + j >= lo && dp + j < hi) gstore8(dp + j, d >> (8 * j));
-  }
-  dp += 4;
-}
-
+// Output: a 128-bit shift register W0..W3 (W0 oldest) whose low B bits are the stream bytes
+// not yet stored, MSB first, above them the last bytes already stored.  Stream byte k sits at
+// slot byte a + k of the dword-aligned origin o (a = slot address & 3, counted as B = 8a
+// phantom bytes at the start), so every complete dword is aligned in memory.
 struct AEnc {
-  u64 low, range, acc, len;
-  u32 nbits;
-  u32 q0, q1, q2, q3, qn;  // settled dwords waiting for the phase boundary
-  uint8_t* dp;             // where q0 goes
+  u64 low, range;
+  u32 W0, W1, W2, W3, B, wpos;  // wpos: origin-relative byte of the next complete dword
+  u32 total, err;
+  double rt;
 };
 
-static __device__ __forceinline__ void aenc_flush(AEnc& e, const uint8_t* lo,
-                                                  const uint8_t* hi) {
-  if (e.qn > 0) put_dword(e.dp, e.q0, lo, hi);
-  if (e.qn > 1) put_dword(e.dp, e.q1, lo, hi);
-  if (e.qn > 2) put_dword(e.dp, e.q2, lo, hi);
-  if (e.qn > 3) put_dword(e.dp, e.q3, lo, hi);
-  e.qn = 0;
+struct AOut {  // per-lane output geometry
+  uint8_t* o;  // slot address & ~3
+  u32 a;       // slot address & 3
+  u32 end;     // a + capacity (clamped to 32 bits): origin-relative end of the slot
+};
+
+// shift the register left by nb bits (0..32) and append the top nb bits of hl
+static __device__ __forceinline__ void out_push(AEnc& e, u32 hl, u32 nb) {
+  e.W0 = hi32((((u64)e.W0 << 32) | e.W1) << nb);
+  e.W1 = hi32((((u64)e.W1 << 32) | e.W2) << nb);
+  e.W2 = hi32((((u64)e.W2 << 32) | e.W3) << nb);
+  e.W3 = hi32((((u64)e.W3 << 32) | hl) << nb);
+  e.B += nb;
 }
 
-static __device__ __forceinline__ void aenc_push(AEnc& e, u32 be, const uint8_t* lo,
-                                                 const uint8_t* hi) {
-  if (e.qn == 4) aenc_flush(e, lo, hi);  // more than 16 B settled within one phase (rare)
-  e.q0 = e.qn == 0 ? be : e.q0;
-  e.q1 = e.qn == 1 ? be : e.q1;
-  e.q2 = e.qn == 2 ? be : e.q2;
-  e.q3 = e.qn == 3 ? be : e.q3;
-  e.qn += 1;
+
+typedef u32 u32x3 __attribute__((ext_vector_type(3)));
+typedef __attribute__((address_space(1))) u32x3 g_u32x3;
+
+// store the complete dwords (B <= 127, so at most 3): the 12 bytes ending at the last of them,
+// the dwords before it being ones already stored (still in the register, unchanged).  Bytes
+// outside [a, end) — the phantom start, or past a too-small slot — are never written.
+static __device__ __forceinline__ void out_flush(AEnc& e, const AOut& g, bool wr) {
+  const u32 cnt = e.B >> 5, sh = e.B & 31u;
+  const u32 v1 = __builtin_bswap32(__builtin_amdgcn_alignbit(e.W0, e.W1, sh));
+  const u32 v2 = __builtin_bswap32(__builtin_amdgcn_alignbit(e.W1, e.W2, sh));
+  const u32 v3 = __builtin_bswap32(__builtin_amdgcn_alignbit(e.W2, e.W3, sh));
+  const u32 st = e.wpos + 4 * cnt - 12;  // wraps below 0 near the start
+  const bool fast = (int)st >= (int)g.a && st + 12 <= g.end;
+  if (wr && fast) {
+    u32x3 v = {v1, v2, v3};
+    *(g_u32x3*)(g.o + st) = v;
+  } else if (wr) {
+    const u32 vv[3] = {v1, v2, v3};
+#pragma unroll
+    for (u32 b = 0; b < 12; ++b) {
+      const u32 pos = st + b;
+      if ((int)pos >= (int)g.a && pos < g.end) gstore8(g.o + pos, vv[b >> 2] >> (8 * (b & 3)));
+    }
+  }
+  e.wpos += 4 * cnt;
+  e.B = sh;
 }
 
-static __device__ __forceinline__ void aenc_byte(AEnc& e, u32 b, const uint8_t* lo,
-                                                 const uint8_t* hi) {
-  e.acc = (e.acc << 8) | b;
-  e.nbits += 8;
-  e.len += 1;
-  if (e.nbits >= 32) {
-    e.nbits -= 32;
-    aenc_push(e, (u32)(e.acc >> e.nbits), lo, hi);
+// param_update (range_coder.rs:53-92) for (c, cum) under total tot: narrowing, closed-form
+// no_carry_expansion (<= 3 bytes: range >= 2^32 here), the settled bytes into the register.
+// Returns whether range_reduction_expansion has work (rare).
+static __device__ __forceinline__ bool enc_code(AEnc& e, u32 cum, u32 c, u32 tot, double rt) {
+  const u64 r = div_total(e.range, tot, rt);
+  e.range = mul_r(r, c);
+  e.low += mul_r(r, cum);
+  const u32 nb = clz32(hi32(e.low) ^ hi32(e.low + e.range)) & 24u;
+  out_push(e, hi32(e.low), nb);
+  e.low <<= nb;
+  e.range <<= nb;
+  return hi32(e.range) < 0x10000u;
+}
+
+// range_reduction_expansion (range_coder.rs:126-135); leaves B <= 31
+static __device__ __forceinline__ void enc_reduce(AEnc& e, const AOut& g, bool wr) {
+  while (e.range < TOP16) {
+    e.range = ~e.low & (TOP16 - 1);
+    if (e.B > 112) out_flush(e, g, wr);
+    out_push(e, hi32(e.low), 8);
+    e.low <<= 8;
+    e.range <<= 8;
+  }
+  out_flush(e, g, wr);
+}
+
+// The tree state of one symbol, prepared and loaded one symbol ahead.  Level l's node on the
+// path of s is at a[l] + ROW(128 >> l), its value v[l] (packed in u16 pairs only at use, so
+// nothing waits for the loads before then); bs/bs1 pack the turn bits of s and s+1 for the
+// level pairs (2k: hi half, 2k+1: lo half), nbm those of ~s.
+struct ESym {
+  u32 a[8];
+  u32 bs[4], bs1[4], nbm[4];
+  u32 s1hi;  // (s + 1) >> 8: cum[256] is the total
+  u32 v[8];
+};
+// keep the symbol bits above level l's turn (s bits 8-l.., at byte bit 7+) and the lane column
+#define LMASK(l) ((0x7F80u & ~(((256u >> (l)) - 1u) << 7)) | 0x7Fu)
+
+typedef __attribute__((address_space(3))) char l_char;
+// LDS byte address a: the kernels' only LDS is the dynamic tree, which starts at 0 (tb, the
+// tree's base, is kept for the halving's pointer accesses and must be 0)
+#define LRD(tb, a) ((u32) * (const __attribute__((address_space(3))) uint16_t*)(uintptr_t)(a))
+#define LWR(tb, a, v) (*(__attribute__((address_space(3))) uint16_t*)(uintptr_t)(a) = (uint16_t)(v))
+
+static __device__ __forceinline__ void esym_prep(ESym& q, u32 s, u32 col) {
+  const u32 X = (s << 7) | col;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) q.a[l] = X & LMASK(l);
+  const u32 u = s | (s << 15), s1 = s + 1, u1 = s1 | (s1 << 15);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    q.bs[k] = (u >> (6 - 2 * k)) & 0x10001u;
+    q.bs1[k] = (u1 >> (6 - 2 * k)) & 0x10001u;
+    q.nbm[k] = q.bs[k] ^ 0x10001u;
+  }
+  q.s1hi = s1 >> 8;
+}
+
+static __device__ __forceinline__ void esym_load(ESym& q, l_char* tb) {
+#pragma unroll
+  for (int l = 0; l < 8; ++l) q.v[l] = LRD(tb, q.a[l] + ROW(128u >> l));
+}
+
+// cum[s] and c[s] = cum[s+1] - cum[s] from the path values; then c[s] += inc: inc on the nodes
+// where the walk turned left, written back as u16s
+static __device__ __forceinline__ void esym_code(const ESym& q, l_char* tb, u32 total, us2 incp,
+                                                 u32& cum, u32& c) {
+  us2 vp[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    vp[k] = (us2){(unsigned short)q.v[2 * k + 1], (unsigned short)q.v[2 * k]};
+  u32 a0 = __builtin_amdgcn_udot2(vp[0], __builtin_bit_cast(us2, q.bs[0]), 0u, false);
+  u32 a1 = __builtin_amdgcn_udot2(vp[0], __builtin_bit_cast(us2, q.bs1[0]), q.s1hi * total,
+                                  false);
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    a0 = __builtin_amdgcn_udot2(vp[k], __builtin_bit_cast(us2, q.bs[k]), a0, false);
+    a1 = __builtin_amdgcn_udot2(vp[k], __builtin_bit_cast(us2, q.bs1[k]), a1, false);
+  }
+  cum = a0;
+  c = a1 - a0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const us2 nv = vp[k] + __builtin_bit_cast(us2, q.nbm[k]) * incp;
+    LWR(tb, q.a[2 * k + 1] + ROW(128u >> (2 * k + 1)), nv.x);
+    LWR(tb, q.a[2 * k] + ROW(128u >> (2 * k)), nv.y);
   }
 }
 
-__global__ __launch_bounds__(AWG) void k_encode_adaptive(
+// one symbol outside the pipelined tile loop (heads, tails, tiles with a bad symbol): the
+// model query and update, param_update, then the period's halving check at symbol index i
+static __device__ __forceinline__ void enc_slow_sym(AEnc& e, const AOut& g, bool wr, l_char* tb,
+                                    uint16_t* tcol, u32 col, u32 s, us2 incp,
+                                    const AdaptParams& p, u32 i) {
+  ESym q;
+  esym_prep(q, s, col);
+  esym_load(q, tb);
+  u32 cum, c;
+  esym_code(q, tb, e.total, incp, cum, c);
+  if (e.B > 96) out_flush(e, g, wr);
+  const u32 tot = e.total;
+  const double rt = e.rt;
+  e.total += p.inc;
+  e.rt = recip(e.total);
+  if (enc_code(e, cum, c, tot, rt)) enc_reduce(e, g, wr);
+  if ((i & p.pmask) == p.pmask && e.total > p.limit) {
+    tree_halve(tcol, e.total);
+    e.rt = recip(e.total);
+  }
+}
+
+// Encoder::finish (encoder.rs:40-46) when fin (8 x left_shift), then the last partial dword;
+// returns the stream length
+static __device__ __forceinline__ u32 enc_finish(AEnc& e, const AOut& g, bool wr, bool fin) {
+  out_flush(e, g, wr);
+  if (fin) {
+    out_push(e, hi32(e.low), 32);
+    out_push(e, (u32)e.low, 32);
+    out_flush(e, g, wr);
+  }
+  const u32 rb = e.B >> 3;
+  for (u32 m = 0; m < rb; ++m) {
+    const u32 pos = e.wpos + m;
+    if (wr && pos >= g.a && pos < g.end) gstore8(g.o + pos, e.W3 >> (e.B - 8 * (m + 1)));
+  }
+  return e.wpos + rb - g.a;
+}
+
+// any of the 16 symbols of a tile outside the alphabet
+static __device__ __forceinline__ bool tile_bad(const u32x4& v, u32 n) {
+  const u32 w[4] = {v.x, v.y, v.z, v.w};
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) bad |= ((w[j >> 2] >> (8 * (j & 3))) & 255u) >= n;
+  return bad;
+}
+
+// the per-lane geometry and state of the encoder kernel
+struct EncLane {
+  AEnc e;
+  AOut g;
+  bool wr, done;
+  u32 hd, nt, tl, nblk, col, k;
+  u64 cap;
+  const u32x4* tp;
+  uint16_t* tcol;
+};
+
+// lanes with all their tiles coded: the tail symbols (per lane, slow) and Encoder::finish
+static __device__ __forceinline__ void enc_lane_end(EncLane& L, l_char* tb, const u32x4& cur, us2 incp,
+                                    const AdaptParams& p, u32 t, u64* out_len, u32* flags) {
+  for (u32 j = 0; j < L.tl && !L.e.err; ++j) {
+    const u32 s = byte_at(cur, j);
+    if (s >= p.n)
+      L.e.err = RC_F_BAD_SYMBOL;  // the reference panics (sample_impl.rs:19)
+    else
+      enc_slow_sym(L.e, L.g, L.wr, tb, L.tcol, L.col, s, incp, p, L.hd + 16 * t + j);
+  }
+  const u32 len = enc_finish(L.e, L.g, L.wr, L.e.err == 0);
+  out_len[L.k] = len;
+  flags[L.k] = L.e.err ? L.e.err : ((u64)len > L.cap ? RC_F_CAPACITY : 0u);
+  L.done = true;
+  L.wr = false;
+}
+
+// The tile loop: T rounds of 16 symbols, every lane at tile t of its own input.  A lane whose
+// tiles run out finishes inside the loop and then runs on dummy input with its writes off.
+// UNI: all lanes share the head length, so the period's halving checks fall on the same
+// symbol in every lane (a scalar test).
+template <bool UNI>
+static __device__ __forceinline__ void enc_tiles(EncLane& L, l_char* tb, us2 incp, const AdaptParams& p, u32 T,
+                                 u32 hd_u, u64* out_len, u32* flags) {
+  auto blk = [&](u32 t) -> u32x4 {
+    return gload16(!L.done && t < L.nblk ? L.tp + t : &g_zero16);
+  };
+  u32x4 cur = blk(0), nxt = blk(1);
+  ESym q;
+  esym_prep(q, cur.x & 255u, L.col);
+  esym_load(q, tb);
+  for (u32 t = 0; t < T; ++t) {
+    const u32x4 pend = blk(t + 2);
+    if (__any((int)(!L.done && t == L.nt))) {
+      if (!L.done && t == L.nt) enc_lane_end(L, tb, cur, incp, p, t, out_len, flags);
+    }
+    // a tile with a symbol outside the alphabet: that lane codes up to it, slowly, and stops
+    if (p.n < 256) {
+      const bool bad = !L.done && tile_bad(cur, p.n);
+      if (__any((int)bad)) {
+        if (bad) {
+          for (u32 j = 0; j < 16 && !L.e.err; ++j) {
+            const u32 s = byte_at(cur, j);
+            if (s >= p.n)
+              L.e.err = RC_F_BAD_SYMBOL;
+            else
+              enc_slow_sym(L.e, L.g, L.wr, tb, L.tcol, L.col, s, incp, p, L.hd + 16 * t + j);
+          }
+          out_len[L.k] = enc_finish(L.e, L.g, L.wr, false);
+          flags[L.k] = L.e.err;
+          L.done = true;
+          L.wr = false;
+        }
+      }
+    }
+    const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
+    // symbol index of the tile's first symbol: scalar when UNI; else the per-lane offset of
+    // the first halving check inside the tile, d = (pmask - i0) & pmask
+    const u32 i0 = hd_u + 16 * t;
+    const u32 d = (p.pmask - (L.hd + 16 * t)) & p.pmask;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      u32 cum, c;
+      esym_code(q, tb, L.e.total, incp, cum, c);
+      const u32 tot = L.e.total;
+      const double rt = L.e.rt;
+      L.e.total += p.inc;
+      // the period's halving check after symbol i (adapt_update), before the next reads
+      bool at;
+      if (UNI)
+        at = ((i0 + j) & p.pmask) == p.pmask;
+      else
+        at = ((u32)j & p.pmask) == d;
+      if (!UNI || at) {
+        const bool h = !L.done && at && L.e.total > p.limit;
+        if (__builtin_expect(__any((int)h), 0)) {
+          if (h) tree_halve(L.tcol, L.e.total);
+        }
+      }
+      L.e.rt = recip(L.e.total);
+      const u32 sn = j < 15 ? (w[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 255u : nxt.x & 255u;
+      ESym qn;
+      esym_prep(qn, sn, L.col);
+      esym_load(qn, tb);
+      const bool rare = enc_code(L.e, cum, c, tot, rt);
+      if (__builtin_expect(__any((int)rare), 0)) {
+        if (rare) enc_reduce(L.e, L.g, L.wr);
+      }
+      if ((j & 3) == 3) out_flush(L.e, L.g, L.wr);
+      q = qn;
+    }
+    cur = nxt;
+    nxt = pend;
+  }
+  if (!L.done) enc_lane_end(L, tb, cur, incp, p, T, out_len, flags);
+}
+
+__global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_encode_adaptive(
     AdaptParams p, const uint8_t* __restrict__ syms, const u64* __restrict__ sym_off,
     u32 n_chunks, uint8_t* __restrict__ out, const u64* __restrict__ out_off,
     u64* __restrict__ out_len, u32* __restrict__ flags) {
   extern __shared__ uint16_t s_tree[];
+  l_char* tb = (l_char*)s_tree;
   const u32 lane = threadIdx.x;
-  const u32 k = blockIdx.x * AWG + lane;
-  const bool live = k < n_chunks;
-  RC_VGPR_FLOOR_64();
-  u64 n = 0, cap = 0;
+  EncLane L;
+  L.k = blockIdx.x * AWG + lane;
+  const bool live = L.k < n_chunks;
+  RC_VGPR_FLOOR_128();
+  u64 n = 0;
+  L.cap = 0;
   const uint8_t* sp = syms;
   uint8_t* lo = out;
   if (live) {
-    const u64 a = sym_off[k], b = out_off[k];
-    n = sym_off[k + 1] - a;
+    const u64 a = sym_off[L.k], b = out_off[L.k];
+    n = sym_off[L.k + 1] - a;
     sp = syms + a;
     lo = out + b;
-    cap = out_off[k + 1] - b;
+    L.cap = out_off[L.k + 1] - b;
   }
-  const uint8_t* hi = lo + cap;
-  uint16_t* t = s_tree + lane;
-  u32* tw = (u32*)(s_tree + (lane & ~1u));
-  const u32 incv = p.inc << (16 * (lane & 1));
-  tree_init(t, p.n);
-  u32 total = p.n, err = 0;
+  L.col = 2 * lane;
+  L.tcol = s_tree + lane;
+  tree_init(L.tcol, p.n);
+  const us2 incp = {(unsigned short)p.inc, (unsigned short)p.inc};
 
-  AEnc e;
+  AEnc& e = L.e;
   e.low = 0;
   e.range = ~0ull;  // RangeCoder::default (range_coder.rs:13-20)
-  e.acc = 0;
-  e.len = 0;
-  e.nbits = 8 * (u32)((uintptr_t)lo & 3);
-  e.q0 = e.q1 = e.q2 = e.q3 = e.qn = 0;
-  e.dp = (uint8_t*)((uintptr_t)lo & ~(uintptr_t)3);
+  e.W0 = e.W1 = e.W2 = e.W3 = 0;
+  e.wpos = 0;
+  e.total = p.n;
+  e.rt = recip(p.n);
+  e.err = 0;
+  L.g.o = (uint8_t*)((uintptr_t)lo & ~(uintptr_t)3);
+  L.g.a = (u32)((uintptr_t)lo & 3);
+  L.g.end = L.g.a + (u32)min(L.cap, (u64)(0xFFFFFF00u - L.g.a));
+  e.B = 8 * L.g.a;
+  L.wr = live;
+  L.done = !live;
 
-  // input window: 16-B blocks cur, nxt (landed) and pend (in flight); a phase's 16 symbols
-  // start at byte (sp & 15) of cur
-  const bool has = live && n > 0;
-  const u32x4* bp = has ? (const u32x4*)((uintptr_t)sp & ~(uintptr_t)15) : &g_zero16;
-  const u32x4* blast = has ? (const u32x4*)((uintptr_t)(sp + n - 1) & ~(uintptr_t)15) : bp;
-  const u32 dsh = ((u32)(uintptr_t)sp >> 2) & 3u, bsh = (u32)(uintptr_t)sp & 3u;
-  u32x4 cur = gload16(bp);
-  bp = bp < blast ? bp + 1 : blast;
-  u32x4 nxt = gload16(bp);
-  bp = bp < blast ? bp + 1 : blast;
-  u32x4 pend = gload16(bp);
+  // symbols [0, hd) until the input is 16-B aligned, then nt 16-symbol tiles, then tl symbols
+  const u32 mis = (u32)(uintptr_t)sp & 15u;
+  L.hd = live ? (u32)min((u64)((16u - mis) & 15u), n) : 0u;
+  L.nt = live ? (u32)((n - L.hd) >> 4) : 0u;
+  L.tl = live ? (u32)((n - L.hd) & 15u) : 0u;
+  L.nblk = L.nt + (L.tl ? 1u : 0u);
+  L.tp = (const u32x4*)(sp + L.hd);
 
-  for (u64 i0 = 0;; i0 += 16) {
-    if (!__any((int)(live && i0 < n && err == 0))) break;  // wave-uniform exit
-    // this phase's 16 symbols, then the boundary I/O: rotate (waits for pend), store, load
-    u32 sw[4];
-    {
-      const u32 v[8] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y, nxt.z, nxt.w};
-#pragma unroll
-      for (u32 q = 0; q < 4; ++q) sw[q] = pick4(v, q, dsh, bsh);
-    }
-    cur = nxt;
-    nxt = pend;
-    aenc_flush(e, lo, hi);
-    bp = bp < blast ? bp + 1 : blast;
-    pend = gload16(bp);
-
-    for (u32 q = 0; q < 4; ++q) {
-      u32 w = sw[0];
-      w = q == 1 ? sw[1] : w;
-      w = q == 2 ? sw[2] : w;
-      w = q == 3 ? sw[3] : w;
-#pragma unroll
-      for (u32 jj = 0; jj < 4; ++jj) {
-        const u64 i = i0 + 4 * q + jj;
-        const bool act = live && i < n && err == 0;
-        bool rare = false;
-        if (act) {
-          const u32 sym = (w >> (8 * jj)) & 255u;
-          if (sym >= p.n) {
-            err = RC_F_BAD_SYMBOL;  // the reference panics (sample_impl.rs:19)
-          } else {
-            u32 cum, c;
-            tree_query(t, sym, total, cum, c);
-            const u64 r = div_total(e.range, total, recip(total));
-            e.range = r * c;   // range_coder.rs:65
-            e.low += r * cum;  // :68-81 (no overflow: r * total <= range)
-            // no_carry_expansion in closed form; range >= 2^32 here, so <= 3 bytes settle
-            const u32 x = hi32(e.low) ^ hi32(e.low + e.range);
-            const u32 nb = (u32)__builtin_clz(x) & 24u;
-            e.acc = (e.acc << nb) | (u32)(((u64)hi32(e.low) << nb) >> 32);
-            e.low <<= nb;
-            e.range <<= nb;
-            e.nbits += nb;
-            e.len += nb >> 3;
-            if (e.nbits >= 32) {
-              e.nbits -= 32;
-              aenc_push(e, (u32)(e.acc >> e.nbits), lo, hi);
-            }
-            rare = hi32(e.range) < 0x10000u;
-            tree_add(tw, sym, incv);
-            total += p.inc;
-          }
-        }
-        if (__builtin_expect(__any((int)rare), 0)) {
-          if (rare) {
-            while (e.range < TOP16) {  // range_reduction_expansion (range_coder.rs:126-135)
-              e.range = ~e.low & (TOP16 - 1);
-              aenc_byte(e, (u32)(e.low >> 56), lo, hi);
-              e.low <<= 8;
-              e.range <<= 8;
-            }
-          }
-        }
-        if (((u32)i & p.pmask) == p.pmask) {  // wave-uniform: the period's halving check
-          const bool h = act && err == 0 && total > p.limit;
-          if (__any((int)h)) {
-            if (h) tree_halve(t, total);
-          }
-        }
+  if (__any((int)(L.hd > 0))) {  // head (per lane, slow)
+    const u32x4 hb = gload16(L.hd > 0 ? (const u32x4*)(sp - mis) : &g_zero16);
+    for (u32 j = 0; __any((int)(j < L.hd && !e.err)); ++j) {
+      if (j < L.hd && !e.err) {
+        const u32 s = byte_at(hb, mis + j);
+        if (s >= p.n)
+          e.err = RC_F_BAD_SYMBOL;  // the reference panics (sample_impl.rs:19)
+        else
+          enc_slow_sym(e, L.g, L.wr, tb, L.tcol, L.col, s, incp, p, j);
       }
+    }
+    if (live && e.err) {
+      out_len[L.k] = enc_finish(e, L.g, L.wr, false);
+      flags[L.k] = e.err;
+      L.done = true;
+      L.wr = false;
     }
   }
+  out_flush(e, L.g, L.wr);  // B <= 31 for the tile loop
 
-  if (live) {
-    if (err == 0) {
-      for (u32 j = 0; j < 8; ++j) {  // Encoder::finish (encoder.rs:40-46): 8 x left_shift
-        aenc_byte(e, (u32)(e.low >> 56), lo, hi);
-        e.low <<= 8;
-      }
-      aenc_flush(e, lo, hi);
-      for (u32 m = 0; m < e.nbits / 8; ++m) {  // the last partial dword
-        uint8_t* a = e.dp + m;
-        if (a >= lo && a < hi) gstore8(a, (u32)(e.acc >> (e.nbits - 8 * (m + 1))));
-      }
-      err = e.len > cap ? RC_F_CAPACITY : 0u;
-    }
-    out_len[k] = e.len;
-    flags[k] = err;
-  }
+  const u32 T = wave_max(L.done ? 0u : L.nt);
+  const u32 hmin = wave_min(L.done ? 16u : L.hd), hmax = wave_max(L.done ? 0u : L.hd);
+  if (hmin >= hmax)
+    enc_tiles<true>(L, tb, incp, p, T, hmax, out_len, flags);
+  else
+    enc_tiles<false>(L, tb, incp, p, T, 0, out_len, flags);
 }
 
 // ------------------------------------------------------------------------------------------
 // Decoder
 // ------------------------------------------------------------------------------------------
 
-// The code of one lane: r[0..fill) are stream dwords (memory order), byte cpos at offset off
-// of r[0]; pend is the 16-B block after them, loaded one phase ahead.
+// The code of one lane: r[0..fill) are stream dwords (memory order), the read position at
+// byte off of r[0]; pend is the 16-B block after them, loaded one phase ahead.
 struct Win {
   u32 r[8];
   u32 off, fill;
@@ -359,160 +571,305 @@ struct Win {
   const u32x4* plast;  // last 16-B block holding a code byte
 };
 
-// the next kb (0..4) code bytes, big-endian (Decoder::shift_left_buffer, decoder.rs:31-35);
-// needs fill >= 2
-static __device__ __forceinline__ u32 win_take(Win& w, u32 kb) {
-  const u32 v = __builtin_bswap32(__builtin_amdgcn_alignbyte(w.r[1], w.r[0], w.off));
-  const u32 res = kb ? v >> (32 - 8 * kb) : 0u;
-  w.off += kb;
-  const bool sh = w.off >= 4;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) w.r[i] = sh ? w.r[i + 1] : w.r[i];
-  w.off -= sh ? 4u : 0u;
-  w.fill -= sh ? 1u : 0u;
-  return res;
+// the 4 code bytes at the read position, big-endian (needs fill >= 2)
+static __device__ __forceinline__ u32 win_peek(const Win& w) {
+  return __builtin_bswap32(__builtin_amdgcn_alignbyte(w.r[1], w.r[0], w.off));
 }
 
-// r[fill .. fill + 4) = pend (fill <= 4), and advance to the next block
-static __device__ __forceinline__ void win_append(Win& w) {
-  const u32 pv[4] = {w.pend.x, w.pend.y, w.pend.z, w.pend.w};
+// consume kb <= 3 bytes (Decoder::shift_left_buffer, decoder.rs:31-35)
+static __device__ __forceinline__ void win_adv(Win& w, u32 kb) {
+  const u32 o = w.off + kb;
+  const u32 sh = o >> 2;  // 0 or 1: a whole dword consumed
+  const u32 m = 0u - sh;
 #pragma unroll
-  for (u32 i = 0; i < 8; ++i) {
-    const u32 d = i - w.fill;  // wraps for i < fill
-    u32 v = pv[0];
-    v = d == 1 ? pv[1] : v;
-    v = d == 2 ? pv[2] : v;
-    v = d == 3 ? pv[3] : v;
-    w.r[i] = d < 4 ? v : w.r[i];
+  for (int i = 0; i < 7; ++i) w.r[i] = msel(m, w.r[i + 1], w.r[i]);
+  w.off = o & 3u;
+  w.fill -= sh;
+}
+
+// r[fill .. fill + 4) = pend (fill <= 4), and advance to the next block: pend shifted up by
+// fill slots (a 3-stage barrel on fill's bits), merged above the valid dwords
+static __device__ __forceinline__ void win_append(Win& w) {
+  const u32 f = w.fill;
+  const u32 m1 = 0u - (f & 1u), m2 = 0u - ((f >> 1) & 1u), m4 = 0u - ((f >> 2) & 1u);
+  const u32 p[4] = {w.pend.x, w.pend.y, w.pend.z, w.pend.w};
+  u32 a[5], b[7], c[8];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) a[i] = msel(m1, i >= 1 ? p[i - 1] : 0u, i < 4 ? p[i] : 0u);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) b[i] = msel(m2, i >= 2 ? a[i - 2] : 0u, i < 5 ? a[i] : 0u);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) c[i] = msel(m4, i >= 4 ? b[i - 4] : 0u, i < 7 ? b[i] : 0u);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const u32 keep = (u32)((int)((u32)i - f) >> 31);  // i < fill
+    w.r[i] = msel(keep, w.r[i], c[i]);
   }
   w.fill += 4;
   w.pnx = w.pnx < w.plast ? w.pnx + 1 : w.plast;
 }
 
-// the ~x * total / range hint (relative error ~2^-21): both shifted by clz(range)
-static __device__ __forceinline__ u32 freq_hint(u64 x, u64 range, u32 total) {
-  const u32 sh = (u32)__builtin_clz(hi32(range));
-  const float X = (float)hi32(x << sh), R = (float)hi32(range << sh);
-  return (u32)fminf(X * ((float)total * __builtin_amdgcn_rcpf(R)), 4.0e9f);
+// u32 -> f32 and f32 -> u32 (saturating) as single instructions
+static __device__ __forceinline__ float cvt_f32(u32 v) {
+  float f;
+  asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"(v));
+  return f;
+}
+static __device__ __forceinline__ u32 cvt_u32_sat(float f) {
+  u32 v;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(v) : "v"(f));
+  return v;
 }
 
 struct ADec {
-  u64 low, range, data, used;
-  u32 total, err;
+  u64 low, range, x;  // x = Decoder::data - lower_bound (mod 2^64): all find_index needs
+  u32 total, used;    // used: code bytes consumed (8 primed + shifted in)
+  float tf;           // (float)total
+  double rt;          // ~1 / total
+  u32 L0, L1a, L1b, L2a, L2b, L2c, L2d;  // tree levels 0-2 (fixed nodes), read one symbol ahead
 };
 
-// Decoder::decode (decoder.rs:38-54) with FreqTable::find_index (sample_impl.rs:27-45) and
-// the model update; returns the symbol.  Wave-uniform call sites only (rare branches).
-static __device__ __forceinline__ u32 adec_sym(ADec& d, Win& w, bool act, const uint16_t* t,
-                                               u32* tw, u32 incv, const AdaptParams& p,
-                                               u64 clen) {
-  if (__builtin_expect(__any((int)(act && w.fill < 2)), 0)) {  // the window ran short (rare)
-    if (act && w.fill < 2) {
+static __device__ __forceinline__ void dec_preread(ADec& d, l_char* tb, u32 col) {
+  d.L0 = LRD(tb, col + ROW(128));
+  d.L1a = LRD(tb, col + ROW(64));
+  d.L1b = LRD(tb, col + ROW(192));
+  d.L2a = LRD(tb, col + ROW(32));
+  d.L2b = LRD(tb, col + ROW(96));
+  d.L2c = LRD(tb, col + ROW(160));
+  d.L2d = LRD(tb, col + ROW(224));
+}
+
+// The walk for target q < total: symbol s, cum[s], c[s], and per level the visited node's
+// row base P[l] (its node at P[l] + ROW(128 >> l)) and updated value nv[l] (+inc on a left turn)
+struct DWalk {
+  u32 s, cum, c;
+  u32 nv[8], P[8];
+};
+
+static __device__ __forceinline__ void dec_walk(DWalk& w, const ADec& d, l_char* tb, u32 q,
+                                                u32 col, u32 inc) {
+  u32 rem = q, b = d.total, P = col;
+  u32 m[8];  // ~0: the walk turned left at that level (rem < node)
+#define RC_LEVEL(l, V)                                   \
+  {                                                      \
+    const u32 v_ = (V), d_ = rem - v_;                   \
+    m[l] = (u32)((int)d_ >> 31);                         \
+    w.nv[l] = v_ + (inc & m[l]);                         \
+    w.P[l] = P;                                          \
+    rem = min(rem, d_);                                  \
+    b = msel(m[l], v_, b - v_);                          \
+    P |= ~m[l] & ((128u >> (l)) * 128u);                 \
+  }
+  RC_LEVEL(0, d.L0)
+  RC_LEVEL(1, msel(m[0], d.L1a, d.L1b))
+  {
+    const u32 t0 = msel(m[0], d.L2a, d.L2c), t1 = msel(m[0], d.L2b, d.L2d);
+    RC_LEVEL(2, msel(m[1], t0, t1))
+  }
+  {  // levels 3-5: one 7-node read below P
+    const u32 r3 = LRD(tb, P + ROW(16)), r4a = LRD(tb, P + ROW(8)), r4b = LRD(tb, P + ROW(24));
+    const u32 r5a = LRD(tb, P + ROW(4)), r5b = LRD(tb, P + ROW(12));
+    const u32 r5c = LRD(tb, P + ROW(20)), r5d = LRD(tb, P + ROW(28));
+    RC_LEVEL(3, r3)
+    RC_LEVEL(4, msel(m[3], r4a, r4b))
+    const u32 u0 = msel(m[3], r5a, r5c), u1 = msel(m[3], r5b, r5d);
+    RC_LEVEL(5, msel(m[4], u0, u1))
+  }
+  {  // levels 6-7: one 3-node read
+    const u32 r6 = LRD(tb, P + ROW(2)), r7a = LRD(tb, P + ROW(1)), r7b = LRD(tb, P + ROW(3));
+    RC_LEVEL(6, r6)
+    RC_LEVEL(7, msel(m[6], r7a, r7b))
+  }
+#undef RC_LEVEL
+  w.s = (P - col) >> 7;
+  w.cum = q - rem;
+  w.c = b;
+}
+
+// c[s] += inc on the walked path
+static __device__ __forceinline__ void dec_update(const DWalk& w, l_char* tb) {
+#pragma unroll
+  for (int l = 0; l < 8; ++l) LWR(tb, w.P[l] + ROW(128u >> l), w.nv[l]);
+}
+
+// Decoder::decode (decoder.rs:38-54) with FreqTable::find_index (sample_impl.rs:27-45) and the
+// model update; returns the symbol.  Wave-uniform call sites only (rare branches inside).
+// the period's halving check after symbol i (adapt_update)
+static __device__ __forceinline__ void dec_halve(ADec& d, l_char* tb, uint16_t* tcol, u32 col) {
+  tree_halve(tcol, d.total);
+}
+
+// at: symbol i is a period end ((i + 1) % period == 0); uni: at is wave-uniform
+template <bool UNI>
+static __device__ __forceinline__ u32 dec_step(ADec& d, Win& w, l_char* tb, u32 col,
+                                               uint16_t* tcol, const AdaptParams& p, bool at) {
+  if (__builtin_expect(__any((int)(w.fill < 2)), 0)) {  // the window ran short (rare)
+    if (w.fill < 2) {
       win_append(w);
       w.pend = gload16(w.pnx);
     }
   }
-  bool rare = false, bad = false;
-  u32 sym = 0, cum = 0, c = 0;
-  u64 r = 0, x = 0;
-  if (act) {
-    x = d.data - d.low;
-    // walk from the hint while the exact division runs; the interval check decides
-    sym = tree_find(t, min(freq_hint(x, d.range, d.total), d.total - 1), d.total, cum, c);
-    r = div_total(d.range, d.total, recip(d.total));
-    const u64 a = r * cum;
-    bad = a > x || x - a >= r * c;  // (for x >= r * total the answer is n - 1: exact path)
-  }
-  if (__builtin_expect(__any((int)bad), 0)) {
-    if (bad) {  // exact rfreq = min(x / r, total - 1), then the walk
-      u32 q = d.total - 1;
-      if (x < r * d.total) {
-        q = min(freq_hint(x, d.range, d.total), d.total - 1);
-        u64 a = r * q;
-        while (a > x) {
-          --q;
+  const u32 nb4 = win_peek(w);
+  // hint q ~ x * total / range from the high halves (range >= 2^48: relative error <= 2^-15)
+  const float X = cvt_f32(hi32(d.x)), R = cvt_f32(hi32(d.range));
+  const u32 q = min(cvt_u32_sat(X * (d.tf * __builtin_amdgcn_rcpf(R))), d.total - 1);
+  const u64 r = div_total(d.range, d.total, d.rt);
+  DWalk wk;
+  dec_walk(wk, d, tb, q, col, p.inc);
+  u64 A = mul_r(r, wk.cum), B = mul_r(r, wk.c);
+  u64 dx = sub64(d.x, A);
+  // exact check r*cum <= x < r*(cum+c) as one unsigned test (A + B <= range: a wrapped x - A
+  // is >= B)
+  if (__builtin_expect(__any((int)(dx >= B)), 0)) {
+    if (dx >= B) {  // exact rfreq = min(x / r, total - 1), then the walk again
+      u32 qe = d.total - 1;
+      if (d.x < mul_r(r, d.total)) {
+        qe = q;
+        u64 a = mul_r(r, qe);
+        while (a > d.x) {
+          --qe;
           a -= r;
         }
-        while (x - a >= r) {
-          ++q;
+        while (d.x - a >= r) {
+          ++qe;
           a += r;
         }
       }
-      sym = tree_find(t, q, d.total, cum, c);
+      dec_walk(wk, d, tb, qe, col, p.inc);
+      A = mul_r(r, wk.cum);
+      B = mul_r(r, wk.c);
+      dx = sub64(d.x, A);
     }
   }
-  if (act) {
-    d.low += r * cum;
-    d.range = r * c;
-    const u32 kb = (u32)__clzll(d.low ^ (d.low + d.range)) >> 3;  // <= 3: range >= 2^32
-    d.low <<= 8 * kb;
-    d.range <<= 8 * kb;
-    d.data = kb ? (d.data << (8 * kb)) | win_take(w, kb) : d.data;
-    d.used += kb;
-    rare = d.range < TOP16;
+  dec_update(wk, tb);
+  d.total += p.inc;
+  if (!UNI || at) {  // the halving check, before the next symbol's tree reads
+    const bool h = at && d.total > p.limit;
+    if (__builtin_expect(__any((int)h), 0)) {
+      if (h) tree_halve(tcol, d.total);
+    }
   }
-  if (__builtin_expect(__any((int)rare), 0)) {
-    if (rare) {
-      while (d.range < TOP16) {  // range_reduction_expansion (range_coder.rs:126-135)
-        d.range = ~d.low & (TOP16 - 1);
-        d.low <<= 8;
-        d.range <<= 8;
-        if (w.fill < 2) {
-          win_append(w);
-          w.pend = gload16(w.pnx);
-        }
-        d.data = (d.data << 8) | win_take(w, 1);
-        d.used += 1;
+  dec_preread(d, tb, col);
+  d.tf = (float)d.total;
+  d.rt = recip(d.total);
+  // param_update (range_coder.rs:53-92), closed form (<= 3 bytes: range >= 2^32 here)
+  d.low += A;
+  d.range = B;
+  const u32 k8 = clz32(hi32(d.low) ^ hi32(d.low + d.range)) & 24u;
+  d.low <<= k8;
+  d.range <<= k8;
+  // data' = data << k8 | bytes and low' = (low + A) << k8: x' = (x - A) << k8 | bytes
+  d.x = ((u64)hi32(dx << k8) << 32) | hi32((((u64)(u32)dx) << 32 | nb4) << k8);
+  win_adv(w, k8 >> 3);
+  d.used += k8 >> 3;
+  if (__builtin_expect(__any((int)(hi32(d.range) < 0x10000u)), 0)) {
+    while (d.range < TOP16) {  // range_reduction_expansion (range_coder.rs:126-135)
+      d.range = ~d.low & (TOP16 - 1);
+      d.low <<= 8;
+      d.range <<= 8;
+      if (w.fill < 2) {
+        win_append(w);
+        w.pend = gload16(w.pnx);
       }
+      d.x = (d.x << 8) | (win_peek(w) >> 24);
+      win_adv(w, 1);
+      d.used += 1;
     }
   }
-  if (act) {
-    if (d.used > clen) {
-      d.err = RC_F_TRUNCATED;  // shift_left_buffer's pop_front panics (decoder.rs:33)
-    } else {
-      tree_add(tw, sym, incv);
-      d.total += p.inc;
-    }
-  }
-  return sym;
+  return wk.s;
 }
 
-__global__ __launch_bounds__(AWG) void k_decode_adaptive(
+struct DecLane {
+  ADec d;
+  Win w;
+  bool done;
+  u32 hd, nt, tl, col, k;
+  u64 clen;
+  uint8_t* op;
+  uint16_t* tcol;
+};
+
+// lanes with all their tiles decoded: the tail symbols (per lane) and the flag
+static __device__ __forceinline__ void dec_lane_end(DecLane& L, l_char* tb, const AdaptParams& p, u32 t,
+                                    u32* flags) {
+  for (u32 j = 0; j < L.tl; ++j) {
+    const u32 i = L.hd + 16 * t + j;
+    gstore8(L.op + i, dec_step<false>(L.d, L.w, tb, L.col, L.tcol, p, (i & p.pmask) == p.pmask));
+  }
+  // shift_left_buffer panics once more bytes are needed than the stream holds (decoder.rs:33)
+  flags[L.k] = (u64)L.d.used > L.clen ? RC_F_TRUNCATED : 0u;
+  L.done = true;
+}
+
+template <bool UNI>
+static __device__ __forceinline__ void dec_tiles(DecLane& L, l_char* tb, const AdaptParams& p, u32 T, u32 hd_u,
+                                 u32* flags) {
+  for (u32 t = 0; t < T; ++t) {
+    if (__any((int)(!L.done && t == L.nt))) {
+      if (!L.done && t == L.nt) dec_lane_end(L, tb, p, t, flags);
+    }
+    const u32 i0 = hd_u + 16 * t;
+    const u32 dd = (p.pmask - (L.hd + 16 * t)) & p.pmask;
+    u32 o[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if ((j & 7) == 0) {  // window phase: consume pend (the only wait), load the next block
+        if (L.w.fill <= 4) win_append(L.w);
+        L.w.pend = gload16(L.w.pnx);
+      }
+      bool at;
+      if (UNI)
+        at = ((i0 + j) & p.pmask) == p.pmask;
+      else
+        at = !L.done && ((u32)j & p.pmask) == dd;
+      o[j >> 2] |= dec_step<UNI>(L.d, L.w, tb, L.col, L.tcol, p, at) << (8 * (j & 3));
+    }
+    if (!L.done) gstore128(L.op + L.hd + 16 * t, (u32x4){o[0], o[1], o[2], o[3]});
+  }
+  if (!L.done) dec_lane_end(L, tb, p, T, flags);
+}
+
+__global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_decode_adaptive(
     AdaptParams p, const uint8_t* __restrict__ code, const u64* __restrict__ code_off,
     const u64* __restrict__ code_len, uint8_t* __restrict__ syms_out,
     const u64* __restrict__ sym_off, u32 n_chunks, u32* __restrict__ flags) {
   extern __shared__ uint16_t s_tree[];
+  l_char* tb = (l_char*)s_tree;
   const u32 lane = threadIdx.x;
-  const u32 k = blockIdx.x * AWG + lane;
-  const bool live = k < n_chunks;
-  RC_VGPR_FLOOR_112();
-  u64 n = 0, clen = 0;
+  DecLane L;
+  L.k = blockIdx.x * AWG + lane;
+  const bool live = L.k < n_chunks;
+  RC_VGPR_FLOOR_144();
+  u64 n = 0;
+  L.clen = 0;
   const uint8_t* cp = code;
-  uint8_t* op = syms_out;
+  L.op = syms_out;
   if (live) {
-    cp = code + code_off[k];
-    clen = code_len[k];
-    const u64 a = sym_off[k];
-    n = sym_off[k + 1] - a;
-    op = syms_out + a;
+    cp = code + code_off[L.k];
+    L.clen = code_len[L.k];
+    const u64 a = sym_off[L.k];
+    n = sym_off[L.k + 1] - a;
+    L.op = syms_out + a;
   }
-  ADec d;
-  d.err = live && clen < 8 ? RC_F_TRUNCATED : 0u;  // Decoder::new panics (decoder.rs:21)
-  uint16_t* t = s_tree + lane;
-  u32* tw = (u32*)(s_tree + (lane & ~1u));
-  const u32 incv = p.inc << (16 * (lane & 1));
-  tree_init(t, p.n);
+  const bool trunc0 = live && L.clen < 8;  // Decoder::new panics (decoder.rs:21)
+  if (trunc0) flags[L.k] = RC_F_TRUNCATED;
+  L.done = !live || trunc0;
+  L.col = 2 * lane;
+  L.tcol = s_tree + lane;
+  tree_init(L.tcol, p.n);
+  ADec& d = L.d;
   d.total = p.n;
+  d.tf = (float)p.n;
+  d.rt = recip(p.n);
   d.low = 0;
   d.range = ~0ull;
-  d.data = 0;
   d.used = 8;
 
   // code window: the first two 16-B blocks, from the dword holding the first byte
-  const bool has = live && d.err == 0;
-  Win w;
+  Win& w = L.w;
+  const bool has = !L.done;
   const u32x4* b0 = has ? (const u32x4*)((uintptr_t)cp & ~(uintptr_t)15) : &g_zero16;
-  w.plast = has ? (const u32x4*)((uintptr_t)(cp + clen - 1) & ~(uintptr_t)15) : b0;
+  w.plast = has ? (const u32x4*)((uintptr_t)(cp + L.clen - 1) & ~(uintptr_t)15) : b0;
   {
     const u32x4 B0 = gload16(b0);
     const u32x4 B1 = gload16(b0 < w.plast ? b0 + 1 : w.plast);
@@ -534,66 +891,35 @@ __global__ __launch_bounds__(AWG) void k_decode_adaptive(
     w.off = (u32)(uintptr_t)cp & 3u;
     w.pnx = b0 + 2 <= w.plast ? b0 + 2 : w.plast;
     w.pend = gload16(w.pnx);
-    const u32 d0 = win_take(w, 4);
-    d.data = ((u64)d0 << 32) | win_take(w, 4);
-  }
-
-  // output: head bytes until op is 8-B aligned, 8-symbol phases, then the tail bytes.  (A
-  // phase of 8 keeps the 8-dword window fed without the short-window path up to ~1.5 B per
-  // symbol: an append needs fill <= 4, and a phase then consumes at most 3 dwords.)
-  const u64 head = min((u64)((8 - ((uintptr_t)op & 7)) & 7), n);
-  u64 i = 0;
-  for (; __any((int)(live && i < head && d.err == 0)); ++i) {
-    const bool act = live && i < head && d.err == 0;
-    const u32 sym = adec_sym(d, w, act, t, tw, incv, p, clen);
-    if (act && d.err == 0) gstore8(op + i, sym);
-    const bool h = act && d.err == 0 && ((u32)i & p.pmask) == p.pmask && d.total > p.limit;
-    if (__any((int)h)) {
-      if (h) tree_halve(t, d.total);
-    }
-  }
-  i = head;  // every lane, at its own symbol index from here on
-  while (__any((int)(live && i + 8 <= n && d.err == 0))) {
-    const bool lact = live && i + 8 <= n && d.err == 0;
-    u32 o0 = 0, o1 = 0;
-    u32 nv = 0;  // symbols decoded in this phase before any error
-    for (u32 q = 0; q < 2; ++q) {
-      u32 wd = 0;
+    // Decoder::new primes 8 bytes (decoder.rs:14-23): two whole dwords from the read position
+    const u32 d0 = win_peek(w);
 #pragma unroll
-      for (u32 jj = 0; jj < 4; ++jj) {
-        const u64 ii = i + 4 * q + jj;
-        const bool act = lact && d.err == 0;
-        wd |= adec_sym(d, w, act, t, tw, incv, p, clen) << (8 * jj);
-        const bool ok = act && d.err == 0;
-        nv += ok ? 1u : 0u;
-        const bool h = ok && ((u32)ii & p.pmask) == p.pmask && d.total > p.limit;
-        if (__any((int)h)) {
-          if (h) tree_halve(t, d.total);
-        }
-      }
-      o0 = q == 0 ? wd : o0;
-      o1 = q == 1 ? wd : o1;
-    }
-    // boundary: consume pend (the only wait), store the block, load the next one
-    if (lact && w.fill <= 4) win_append(w);
-    if (lact && nv == 8) {
-      *(__attribute__((address_space(1))) u64*)(op + i) = ((u64)o1 << 32) | o0;
-    } else if (lact) {  // truncated inside the phase: the symbols before the error
-      for (u32 j = 0; j < nv; ++j) gstore8(op + i + j, (j < 4 ? o0 : o1) >> (8 * (j & 3)));
-    }
-    w.pend = gload16(w.pnx);
-    i += lact ? 8u : 0u;
+    for (int i = 0; i < 7; ++i) w.r[i] = w.r[i + 1];
+    const u32 d1 = win_peek(w);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) w.r[i] = w.r[i + 1];
+    w.fill -= 2;
+    d.x = ((u64)d0 << 32) | d1;  // data - low with low = 0
   }
-  for (; __any((int)(live && i < n && d.err == 0)); ++i) {  // tail
-    const bool act = live && i < n && d.err == 0;
-    const u32 sym = adec_sym(d, w, act, t, tw, incv, p, clen);
-    if (act && d.err == 0) gstore8(op + i, sym);
-    const bool h = act && d.err == 0 && ((u32)i & p.pmask) == p.pmask && d.total > p.limit;
-    if (__any((int)h)) {
-      if (h) tree_halve(t, d.total);
+  dec_preread(d, tb, L.col);
+
+  // output: symbols [0, hd) until it is 16-B aligned (per lane, byte stores), nt 16-symbol
+  // tiles, then tl symbols
+  const u32 mis = (u32)(uintptr_t)L.op & 15u;
+  L.hd = live ? (u32)min((u64)((16u - mis) & 15u), n) : 0u;
+  L.nt = live ? (u32)((n - L.hd) >> 4) : 0u;
+  L.tl = live ? (u32)((n - L.hd) & 15u) : 0u;
+  for (u32 j = 0; __any((int)(j < L.hd && !L.done)); ++j) {
+    if (j < L.hd && !L.done) {
+      gstore8(L.op + j, dec_step<false>(d, w, tb, L.col, L.tcol, p, (j & p.pmask) == p.pmask));
     }
   }
-  if (live) flags[k] = d.err;
+  const u32 T = wave_max(L.done ? 0u : L.nt);
+  const u32 hmin = wave_min(L.done ? 16u : L.hd), hmax = wave_max(L.done ? 0u : L.hd);
+  if (hmin >= hmax)
+    dec_tiles<true>(L, tb, p, T, hmax, flags);
+  else
+    dec_tiles<false>(L, tb, p, T, 0, flags);
 }
 
 hipError_t rc_adaptive_encode_launch(hipStream_t stream, const AdaptParams& p,

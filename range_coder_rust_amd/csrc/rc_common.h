@@ -22,6 +22,8 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 #define RC_VGPR_FLOOR_96() asm volatile("; vgpr floor 96" ::: "v95")
 #define RC_VGPR_FLOOR_112() asm volatile("; vgpr floor 112" ::: "v111")
 #define RC_VGPR_FLOOR_128() asm volatile("; vgpr floor 128" ::: "v127")
+#define RC_VGPR_FLOOR_144() asm volatile("; vgpr floor 144" ::: "v143")
+#define RC_VGPR_FLOOR_160() asm volatile("; vgpr floor 160" ::: "v159")
 
 static __device__ __forceinline__ u32 hi32(u64 v) { return (u32)(v >> 32); }
 
