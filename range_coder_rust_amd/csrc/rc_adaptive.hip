@@ -68,16 +68,6 @@ static __device__ __forceinline__ u64 div_total(u64 v, u32 t, double rt) {
   return ((u64)qh << 32) | ql;
 }
 
-// a - b (64-bit) with the borrow in an SGPR pair rather than VCC
-static __device__ __forceinline__ u64 sub64(u64 a, u64 b) {
-  u32 lo, hi;
-  u64 c;
-  asm("v_sub_co_u32_e64 %0, %2, %3, %4\n\tv_subb_co_u32_e64 %1, %2, %5, %6, %2"
-      : "=&v"(lo), "=&v"(hi), "=&s"(c)
-      : "v"((u32)a), "v"((u32)b), "v"(hi32(a)), "v"(hi32(b)));
-  return ((u64)hi << 32) | lo;
-}
-
 // (m & a) | (~m & b) for a mask m of 0 / ~0: one v_bfi_b32.  The empty asm hides that m is a
 // mask, or the compiler turns this back into v_cmp + v_cndmask_b32 on VCC.
 static __device__ __forceinline__ u32 msel(u32 m, u32 a, u32 b) {

@@ -27,6 +27,17 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
 static __device__ __forceinline__ u32 hi32(u64 v) { return (u32)(v >> 32); }
 
+// a - b (64-bit) with the borrow in an SGPR pair: the compiler's v_subb_co_u32_e32 reads VCC,
+// and a VALU read of VCC costs ~13 extra SIMD cycles on gfx950 (tools/ubench_issue.hip)
+static __device__ __forceinline__ u64 sub64(u64 a, u64 b) {
+  u32 lo, hi;
+  u64 c;
+  asm("v_sub_co_u32_e64 %0, %2, %3, %4\n\tv_subb_co_u32_e64 %1, %2, %5, %6, %2"
+      : "=&v"(lo), "=&v"(hi), "=&s"(c)
+      : "v"((u32)a), "v"((u32)b), "v"(hi32(a)), "v"(hi32(b)));
+  return ((u64)hi << 32) | lo;
+}
+
 // Global (not flat) memory access.  A flat access also counts in lgkmcnt, so every LDS wait
 // would wait for it too; pointers that pass through LDS or integer casts lose their address
 // space and compile to flat unless cast back like this.

@@ -242,15 +242,23 @@ template <int DIV, int SM>
 static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const uint2* s_tab,
                                              uint4 v, bool act, u32 lane, const u32* wring,
                                              const EncOut* wout) {
-  const u32 w[4] = {v.x, v.y, v.z, v.w};
-  uint2 t = s_tab[w[0] & 255u];
+  // the words rotate down (w0 holds the current 4 symbols) instead of being indexed: a rolled
+  // loop would select w[i >> 2] with v_cndmask_b32 on VCC (~13 extra SIMD cycles each)
+  u32 w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+  uint2 t = s_tab[w0 & 255u];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    uint2 tn = t;
-    if (i < 15) tn = s_tab[(w[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 255u];
-    enc_sym<DIV, SM>(e, m, t, act, lane, wring, wout);
-    t = tn;
-    if ((i & 7) == 7) enc_flush(e, lane, wring, wout);
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u32 sn = i < 3 ? (w0 >> (8 * (i + 1))) & 255u : w1 & 255u;
+      const uint2 tn = s_tab[sn];  // (past the tile's end: a harmless extra read)
+      enc_sym<DIV, SM>(e, m, t, act, lane, wring, wout);
+      t = tn;
+    }
+    if (q & 1) enc_flush(e, lane, wring, wout);
+    w0 = w1;
+    w1 = w2;
+    w2 = w3;
   }
 }
 
@@ -432,15 +440,17 @@ struct Dec {
   u32 err;
   u32 pend_ok;           // a 64-B load is in flight in pend[]
   u32* ring;             // this lane's ring column: dword j at ring[j * 64]
-  const uint4* gnext;    // next 16-B block of the stream
-  const uint4* glast;    // last block holding a byte of this chunk (fetch clamp)
+  const uint4* gbase;    // 16-B aligned base of the stream
+  u32 gnext;             // next 16-B block (index from gbase)
+  u32 glast;             // last block holding a byte of this chunk (fetch clamp)
   uint4 pend[4];
 };
 
 static __device__ __forceinline__ void dec_issue(Dec& d) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint4* p = d.gnext + q < d.glast ? d.gnext + q : d.glast;
+    // 32-bit block index clamp (v_min_u32): a 64-bit pointer compare would select on VCC
+    const uint4* p = d.gbase + min(d.gnext + q, d.glast);
     const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;  // global, not flat
     d.pend[q] = make_uint4(v.x, v.y, v.z, v.w);
   }
@@ -599,7 +609,7 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   // exact verification r*cum[s] <= x < r*cum[s+1] as ONE unsigned test: A + B <= range < 2^64,
   // so when A > x the wrapped difference x - A is >= 2^64 - A > B.  The hint is rarely off.
   // (At s = n - 1 the test fails only on corrupt input, x >= r * total: dec_fix keeps s = n-1.)
-  u64 dx = x - A;
+  u64 dx = sub64(x, A);
   if (__builtin_expect(__any((int)(dx >= B)), 0)) {
     if (dx >= B) {
       dec_fix(s, t, A, B, x, r, s_tab, m.n);
@@ -609,7 +619,7 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
         d.err = d.err ? d.err : (d.cpos > d.lim ? RC_F_TRUNCATED : RC_F_CORRUPT);
         B = r;
       }
-      dx = x - A;
+      dx = sub64(x, A);
     }
   }
   // param_update (range_coder.rs:53-92)
@@ -691,8 +701,9 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   d.fill = 0;
   d.pend_ok = 0;
   d.ring = s_ring + wave * DEC_RING_ALLOC * 64 + lane;
-  d.gnext = reinterpret_cast<const uint4*>(cp - a);
-  d.glast = reinterpret_cast<const uint4*>((uintptr_t)(cp + clen - 1) & ~(uintptr_t)15);
+  d.gbase = reinterpret_cast<const uint4*>(cp - a);
+  d.gnext = 0;
+  d.glast = (u32)((a + clen - 1) >> 4);
   d.cpos = a + 8;  // Decoder::new primes 8 bytes (decoder.rs:21)
   d.lim = (u32)(clen < 0xFFFFFF00ull - a ? a + clen : 0xFFFFFF00ull);
   dec_issue(d);
