@@ -431,6 +431,8 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
 // waited for with vmcnt(1) one phase after it was issued.  Lanes that consume faster than the
 // ring covers (rare renormalisation bursts) are refilled synchronously.
 // ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) u32 l_u32;
+
 struct Dec {
   u64 low, range;  // RangeCoder (decoder.rs:6-12)
   u64 x;           // Decoder::data - lower_bound (mod 2^64): all find_index needs (sample_impl.rs:29)
@@ -439,7 +441,7 @@ struct Dec {
   u32 lim;    // cpos > lim: more bytes consumed than the stream holds
   u32 err;
   u32 pend_ok;           // a 64-B load is in flight in pend[]
-  u32* ring;             // this lane's ring column: dword j at ring[j * 64]
+  l_u32* ring;           // this lane's ring column: dword j at ring[j * 64] (LDS pointer)
   const uint4* gbase;    // 16-B aligned base of the stream
   u32 gnext;             // next 16-B block (index from gbase)
   u32 glast;             // last block holding a byte of this chunk (fetch clamp)
@@ -460,7 +462,7 @@ static __device__ __forceinline__ void dec_issue(Dec& d) {
 
 static __device__ __forceinline__ void dec_commit(Dec& d) {
   const u32 j = (d.fill >> 2) & (DEC_RING - 1);
-  u32* rp = d.ring + j * 64;
+  l_u32* rp = d.ring + j * 64;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     rp[(4 * q + 0) * 64] = d.pend[q].x;
@@ -495,7 +497,7 @@ static __device__ __forceinline__ void dec_sync(Dec& d, u32 need) {
 // the 8 code bytes ending at cpos, big-endian (Decoder::new's priming, decoder.rs:14-23)
 static __device__ __forceinline__ u64 dec_read8_before(const Dec& d) {
   const u32 p = d.cpos - 8;
-  const u32* rp = d.ring + ((p >> 2) & (DEC_RING - 1)) * 64;
+  const l_u32* rp = d.ring + ((p >> 2) & (DEC_RING - 1)) * 64;
   const u32 d0 = rp[0], d1 = rp[64], d2 = rp[128];
   const u32 sh = p & 3;
   const u32 w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
@@ -523,6 +525,7 @@ static __device__ __forceinline__ void dec_rare(Dec& d, u32 need) {
 // the exact index: s = #{ j in [1, n-1] : r * cum[j] <= x }  (FreqTable::find_index)
 static __device__ __forceinline__ void dec_fix(u32& s, uint2& t, u64& A, u64& B, u64 x,
                                                         u64 r, const uint2* s_tab, u32 n) {
+  s &= 255u;
   if (A > x) {
     do {
       --s;
@@ -562,12 +565,34 @@ static __device__ __forceinline__ u32 cvt_u32_sat(float f) {
 #define DEC_NEED_SM 12u
 #define DEC_NEED_WIDE 8u
 
+// byte j of w = byte 0 of v, other bytes kept (j = 0: cleared): one v_mov_b32_sdwa
+static __device__ __forceinline__ u32 put_byte(u32 w, u32 v, int j) {
+  switch (j) {
+    case 0:
+      asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0"
+          : "=v"(w) : "v"(v));
+      break;
+    case 1:
+      asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0"
+          : "+v"(w) : "v"(v));
+      break;
+    case 2:
+      asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0"
+          : "+v"(w) : "v"(v));
+      break;
+    default:
+      asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0"
+          : "+v"(w) : "v"(v));
+  }
+  return w;
+}
+
 template <int DIV, int SM, int LUT>
 static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const uint2* s_tab,
                                               const u32* s_lut) {
   // the code bytes at cpos (the ring holds the ones this symbol can settle); they are shifted
   // into x at the end
-  const u32* rp = d.ring + ((d.cpos >> 2) & (DEC_RING - 1)) * 64;
+  const l_u32* rp = d.ring + ((d.cpos >> 2) & (DEC_RING - 1)) * 64;
   const u32 D0 = rp[0], D1 = rp[64];
   const u32 D2 = SM ? 0u : rp[128];
   const u64 x = d.x;
@@ -593,9 +618,10 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   u32 s;
   uint2 t;
   if (LUT) {  // direct table: candidate symbol and its (cum, c) in one LDS read at byte 4q
+    // the LUT is the kernel's first LDS object (address 0): q4 is its LDS byte address
     const u32 q4 = cvt_u32_sat(X * ((4.0f * m.ftotal) * rR)) & (m.lut_max << 2);
-    const u32 ent = *reinterpret_cast<const u32*>(reinterpret_cast<const char*>(s_lut) + q4);
-    s = ent & 255u;
+    const u32 ent = *(const __attribute__((address_space(3))) u32*)(uintptr_t)q4;
+    s = ent;  // the symbol is its low byte (callers take byte 0; dec_fix masks it)
     t = make_uint2((ent >> 8) & 0xFFFu, ent >> 20);
   } else {  // bucket table, then the (cum, c) table
     const u32 qh = cvt_u32_sat(X * (m.ftotal * rR));
@@ -670,10 +696,13 @@ __global__ __launch_bounds__(WG) void k_decode_static(
     ModelArgs m, const uint8_t* __restrict__ code, const u64* __restrict__ code_off,
     const u64* __restrict__ code_len, uint8_t* __restrict__ syms_out,
     const u64* __restrict__ sym_off, u32 n_chunks, u32* __restrict__ flags) {
-  __shared__ uint2 s_tab[256];
-  __shared__ u32 s_ring[WAVES * DEC_RING_ALLOC * 64];
-  extern __shared__ u32 s_lut[];  // lut_max + 1 entries, sized at launch: the WG's LDS
-                                  // footprint sets how many WGs share a CU
+  // All LDS is dynamic, sized at launch (the WG's footprint sets how many WGs share a CU):
+  // the LUT (lut_max + 1 entries) first, at LDS address 0, so a table read is a ds_read at the
+  // hint's byte offset with no base add; then the (cum, c) table and the code rings.
+  extern __shared__ u32 s_dyn[];
+  u32* s_lut = s_dyn;
+  const u32 lut_words = (m.lut_max + 2) & ~1u;  // 8-B aligned s_tab
+  uint2* s_tab = reinterpret_cast<uint2*>(s_dyn + lut_words);
   const u32 tid = threadIdx.x;
   s_tab[tid] = m.tab[tid];
   for (u32 j = tid; j <= m.lut_max; j += WG) s_lut[j] = m.lut[j];
@@ -700,7 +729,8 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   d.err = 0;
   d.fill = 0;
   d.pend_ok = 0;
-  d.ring = s_ring + wave * DEC_RING_ALLOC * 64 + lane;
+  // the ring as a plain LDS address (s_dyn is at 0), one register: no per-access base math
+  d.ring = (l_u32*)(uintptr_t)((lut_words + 512) * 4) + wave * DEC_RING_ALLOC * 64 + lane;
   d.gbase = reinterpret_cast<const uint4*>(cp - a);
   d.gnext = 0;
   d.glast = (u32)((a + clen - 1) >> 4);
@@ -727,7 +757,7 @@ __global__ __launch_bounds__(WG) void k_decode_static(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[q] |= dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut) << (8 * j);
+      for (int j = 0; j < 4; ++j) w[q] = put_byte(w[q], dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut), j);
       if (q < 3) dec_check4<SM>(d);
     }
     ob[b] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -1126,7 +1156,9 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   hipLaunchKernelGGL((k_decode_static<D, S, L>), grid, block, lut_bytes, ctx->cur, m->args, \
                      code, code_off, code_len, syms_out, sym_off, n_chunks, flags)
   const bool dl = m->args.direct != 0;
-  const size_t lut_bytes = (size_t)(m->args.lut_max + 1) * sizeof(u32);
+  // dynamic LDS of k_decode_static: LUT (8-B aligned), the (cum, c) table, the code rings
+  const size_t lut_bytes = ((size_t)(m->args.lut_max + 2) & ~(size_t)1) * sizeof(u32) +
+                           256 * sizeof(uint2) + WAVES * DEC_RING_ALLOC * 64 * sizeof(u32);
 #ifdef RC_DEV_ONLY
   if (m->div != DIV_POW2 || !sm) return RC_E_ARG;
   if (dl) RC_DEC_LAUNCH(DIV_POW2, 1, 1); else RC_DEC_LAUNCH(DIV_POW2, 1, 0);
