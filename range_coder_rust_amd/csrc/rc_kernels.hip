@@ -85,8 +85,15 @@ struct Enc {
                    // dword B >> 5 of the stream is the incomplete one (its ring slot is free)
   u32 fpos;        // byte position of the next unit to store
   u32 err;         // first RC_F_* error of this chunk (SM: OR of staged table flags)
-  u32* ring;       // this lane's ring column: dword j at ring[j * 64]
+  u32 ring;        // LDS byte address of this lane's ring column: dword j at ring + 256 * j.
+                   // The ring holds stream dwords as values (first byte in the top bits);
+                   // the flush rounds byte-swap them on the way out.
 };
+
+// ring dword `slot` of the lane whose column is at LDS byte address `col`
+static __device__ __forceinline__ void ring_put(u32 col, u32 slot, u32 v) {
+  *(__attribute__((address_space(3))) u32*)(uintptr_t)(col + (slot << 8)) = v;
+}
 
 // byte position of the incomplete dword (everything below it has been pushed to the ring)
 static __device__ __forceinline__ u32 enc_wpos(const Enc& e) { return (e.B >> 5) << 2; }
@@ -117,10 +124,10 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
     if (hc) {
       const u32 slot = (fp >> 2) + 4 * g;
       const u32* rp = wring + c;
-      const uint4 v = make_uint4(rp[((slot + 0) & (ENC_RING - 1)) * 64],
-                                 rp[((slot + 1) & (ENC_RING - 1)) * 64],
-                                 rp[((slot + 2) & (ENC_RING - 1)) * 64],
-                                 rp[((slot + 3) & (ENC_RING - 1)) * 64]);
+      const uint4 v = make_uint4(__builtin_bswap32(rp[((slot + 0) & (ENC_RING - 1)) * 64]),
+                                 __builtin_bswap32(rp[((slot + 1) & (ENC_RING - 1)) * 64]),
+                                 __builtin_bswap32(rp[((slot + 2) & (ENC_RING - 1)) * 64]),
+                                 __builtin_bswap32(rp[((slot + 3) & (ENC_RING - 1)) * 64]));
       const EncOut o = wout[c];
       const u32 p0 = fp + 16 * g;
       if (p0 >= o.lo_ok && p0 + 16 <= o.hi_ok) {
@@ -154,8 +161,7 @@ static __device__ __forceinline__ void enc_flush(Enc& e, u32 lane, const u32* wr
 static __device__ __forceinline__ void enc_emit_byte(Enc& e, u32 b) {
   e.acc = (e.acc << 8) | b;
   e.B += 8;
-  if ((e.B & 31) == 0)
-    e.ring[(((e.B >> 5) - 1) & (ENC_RING - 1)) * 64] = __builtin_bswap32((u32)e.acc);
+  if ((e.B & 31) == 0) ring_put(e.ring, ((e.B >> 5) - 1) & (ENC_RING - 1), (u32)e.acc);
 }
 
 // Rare tail of param_update for one lane: the no-carry loop when >= 4 bytes settle
@@ -178,10 +184,15 @@ static __device__ __forceinline__ void enc_rare(Enc& e) {
 // common path without branches.  Returns true when the lane needs enc_rare().  Written for the
 // gfx950 VALU price list (profiles/r01/ubench_valu.txt): 64-bit ops, multiplies, compares and
 // bit-field ops cost ~3.6 cycles per wave, plain 32-bit add/logic/right-shift ~2.
+// SM: 0 wide model; 1 small model (256 <= total <= 2^16) that may hold entries the reference
+// cannot encode; 2 small and complete (256 symbols, every c > 0: nothing to check)
 template <int DIV, int SM>
 static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint2 t) {
   u32 c, cum;
-  if (SM) {  // bad entries were staged as (flag << 24, 1): accumulate, sort out at the end
+  if (SM == 2) {
+    cum = t.x;
+    c = t.y;
+  } else if (SM) {  // bad entries were staged as (flag << 24, 1): accumulate, sort out at the end
     // (as an asm OR: left to itself the compiler defers all the ORs to the end of the loop
     // and spills every table entry)
     asm volatile("v_or_b32 %0, %0, %1" : "+v"(e.err) : "v"(t.x));
@@ -216,9 +227,12 @@ static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint
   e.range <<= nb;
   // push: the slot of the dword that was incomplete before this symbol gets the 32 bits above
   // the (new) incomplete ones; if it is still incomplete the slot is rewritten later
-  const u32 slot = (e.B >> 5) & (ENC_RING - 1);
+  const u32 slot = __builtin_amdgcn_ubfe(e.B, 5, 5);  // (B >> 5) & (ENC_RING - 1): v_bfe_u32
   e.B += nb;
-  e.ring[slot * 64] = __builtin_bswap32((u32)(e.acc >> (e.B & 31u)));
+  ring_put(e.ring, slot, (u32)(e.acc >> (e.B & 31u)));
+  // SM: range >= 2^32 after narrowing, so the high halves differ (z <= 31) and at most 3 bytes
+  // settle; only range_reduction_expansion can be pending
+  if (SM) return hi32(e.range) < 0x10000u;
   return (z > 31u) | (hi32(e.range) < 0x10000u);
 }
 
@@ -298,7 +312,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
     // alphabet: panic) is staged as (flag << 24, c = 1), so the common path only ORs entries
     // together; a chunk whose OR shows a flag is re-scanned for its first error at the end
     uint2 t = m.tab[tid];
-    if (SM && t.y == 0)
+    if (SM == 1 && t.y == 0)
       t = make_uint2((t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ) << 24, 1u);
     s_tab[tid] = t;
   }
@@ -331,7 +345,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   e.B = 8 * a;  // pad bytes in front of the slot (never stored)
   e.fpos = 0;
   e.err = 0;
-  e.ring = s_ring + wave * ENC_RING * 64 + lane;
+  e.ring = (u32)(uintptr_t)(__attribute__((address_space(3))) u32*)(s_ring + wave * ENC_RING * 64 + lane);
 
   const uint8_t* sp = syms + s0;
   u64 head = (64 - ((uintptr_t)sp & 63)) & 63;  // symbols before the first 64-B aligned tile
@@ -405,8 +419,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   const u32 len = (e.B >> 3) - a;
   u32 wend = enc_wpos(e);
   if (e.B & 31) {  // the last, incomplete dword
-    e.ring[((e.B >> 5) & (ENC_RING - 1)) * 64] =
-        __builtin_bswap32((u32)(e.acc << (32 - (e.B & 31))));
+    ring_put(e.ring, (e.B >> 5) & (ENC_RING - 1), (u32)(e.acc << (32 - (e.B & 31))));
     wend += 4;
   }
   // final rounds: the last (partial) units, clipped to the stream end
@@ -414,7 +427,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   if (end < s_out[tid].hi_ok) s_out[tid].hi_ok = end;
   while (__any((int)(e.fpos < wend))) enc_round(e, e.fpos < wend, lane, wring, wout);
   if (live) {
-    if (SM) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
+    if (SM == 1) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
     if (!e.err && (u64)len > cap) e.err = RC_F_CAPACITY;
     out_len[k] = len;
     flags[k] = e.err;
@@ -842,6 +855,7 @@ struct rc_model {
   AdaptParams ap;      // kind 1
   u32 c_host[256];     // kind 0: the c_freq snapshot (container tables, entropy reports)
   u32 period;          // kind 1: as given
+  bool complete;       // kind 0: 256 symbols, every c_freq > 0 (no symbol the coder can reject)
 };
 
 namespace {
@@ -1072,6 +1086,8 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
   mm->ap = AdaptParams{};
   memset(mm->c_host, 0, sizeof mm->c_host);
   for (u32 i = 0; i < n_symbols; ++i) mm->c_host[i] = c_freq[i];
+  mm->complete = n_symbols == 256;
+  for (u32 i = 0; i < n_symbols; ++i) mm->complete = mm->complete && c_freq[i] > 0;
   mm->period = 0;
   *out = mm;
   return RC_OK;
@@ -1119,17 +1135,22 @@ rc_status rc_encode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   }
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
   const bool sm = m->args.total >= 256 && m->args.total <= 65536;
+  const int smv = sm ? (m->complete ? 2 : 1) : 0;
 #define RC_ENC_LAUNCH(D, S)                                                                \
   hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, ctx->cur, m->args, syms,    \
                      sym_off, n_chunks, out, out_off, out_len, flags)
 #ifdef RC_DEV_ONLY  // scratch builds for kernel tuning: the headline variants only
   if (m->div != DIV_POW2 || !sm) return RC_E_ARG;
-  RC_ENC_LAUNCH(DIV_POW2, 1);
+  if (smv == 2) RC_ENC_LAUNCH(DIV_POW2, 2); else RC_ENC_LAUNCH(DIV_POW2, 1);
 #else
   if (m->div == DIV_POW2) {
-    if (sm) RC_ENC_LAUNCH(DIV_POW2, 1); else RC_ENC_LAUNCH(DIV_POW2, 0);
+    if (smv == 2) RC_ENC_LAUNCH(DIV_POW2, 2);
+    else if (smv == 1) RC_ENC_LAUNCH(DIV_POW2, 1);
+    else RC_ENC_LAUNCH(DIV_POW2, 0);
   } else {
-    if (sm) RC_ENC_LAUNCH(DIV_MAGIC, 1); else RC_ENC_LAUNCH(DIV_MAGIC, 0);
+    if (smv == 2) RC_ENC_LAUNCH(DIV_MAGIC, 2);
+    else if (smv == 1) RC_ENC_LAUNCH(DIV_MAGIC, 1);
+    else RC_ENC_LAUNCH(DIV_MAGIC, 0);
   }
 #endif
 #undef RC_ENC_LAUNCH
