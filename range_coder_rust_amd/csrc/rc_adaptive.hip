@@ -11,7 +11,8 @@
 // Layout: one chunk per lane, one wave per workgroup.  Each lane's counts live in LDS as a
 // 255-node tree of u16 (32 KiB per wave, so 5 waves per CU).  Node 256 — the total — lives in a
 // register.  The tree is interleaved by lane, so one node row is one conflict-free 128-B access:
-//     node j (1..255) = the counts of symbols [j - lowbit(j), j),  at byte (j-1)*128 + 2*lane.
+//     node j (1..255) = the counts of symbols [j - lowbit(j), j),  at byte (j-1)*128 + col,
+// col = 4 (lane mod 32) + 2 (lane div 32) (bank-conflict free per 32-lane group).
 // Read top-down, that is the left-subtree-sum tree over the 256 symbols.  For symbol s, level l
 // (0..7) visits node (s & ~(2*step-1)) | step, step = 128 >> l, and turns right iff bit 7-l of s
 // is set.  Read as a Fenwick tree, it turns into counts and back in place for the halving.
@@ -491,8 +492,11 @@ __global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     lo = out + b;
     L.cap = out_off[L.k + 1] - b;
   }
-  L.col = 2 * lane;
-  L.tcol = s_tree + lane;
+  // lane L's u16 at byte 4 (L mod 32) + 2 (L div 32) of each row: a ds_read_u16 / ds_write_b16
+  // serves lanes 0-31 and 32-63 as separate groups, and within a group every lane has its own
+  // bank (lane pairs sharing a dword conflicted 2-way whenever they read different rows)
+  L.col = ((lane & 31u) << 2) | ((lane >> 5) << 1);
+  L.tcol = s_tree + (L.col >> 1);
   tree_init(L.tcol, p.n);
   const us2 incp = {(unsigned short)p.inc, (unsigned short)p.inc};
 
@@ -844,8 +848,11 @@ __global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const bool trunc0 = live && L.clen < 8;  // Decoder::new panics (decoder.rs:21)
   if (trunc0) flags[L.k] = RC_F_TRUNCATED;
   L.done = !live || trunc0;
-  L.col = 2 * lane;
-  L.tcol = s_tree + lane;
+  // lane L's u16 at byte 4 (L mod 32) + 2 (L div 32) of each row: a ds_read_u16 / ds_write_b16
+  // serves lanes 0-31 and 32-63 as separate groups, and within a group every lane has its own
+  // bank (lane pairs sharing a dword conflicted 2-way whenever they read different rows)
+  L.col = ((lane & 31u) << 2) | ((lane >> 5) << 1);
+  L.tcol = s_tree + (L.col >> 1);
   tree_init(L.tcol, p.n);
   ADec& d = L.d;
   d.total = p.n;
