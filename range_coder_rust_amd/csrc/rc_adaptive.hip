@@ -258,6 +258,7 @@ struct ESym {
   u32 a[8];
   u32 bs[4], bs1[4], nbm[4];
   u32 s1hi;  // (s + 1) >> 8: cum[256] is the total
+  u32 s;
   u32 v[8];
 };
 // keep the symbol bits above level l's turn (s bits 8-l.., at byte bit 7+) and the lane column
@@ -281,6 +282,7 @@ static __device__ __forceinline__ void esym_prep(ESym& q, u32 s, u32 col) {
     q.nbm[k] = q.bs[k] ^ 0x10001u;
   }
   q.s1hi = s1 >> 8;
+  q.s = s;
 }
 
 static __device__ __forceinline__ void esym_load(ESym& q, l_char* tb) {
@@ -314,28 +316,6 @@ static __device__ __forceinline__ void esym_code(const ESym& q, l_char* tb, u32 
   }
 }
 
-// one symbol outside the pipelined tile loop (heads, tails, tiles with a bad symbol): the
-// model query and update, param_update, then the period's halving check at symbol index i
-static __device__ __forceinline__ void enc_slow_sym(AEnc& e, const AOut& g, bool wr, l_char* tb,
-                                    uint16_t* tcol, u32 col, u32 s, us2 incp,
-                                    const AdaptParams& p, u32 i) {
-  ESym q;
-  esym_prep(q, s, col);
-  esym_load(q, tb);
-  u32 cum, c;
-  esym_code(q, tb, e.total, incp, cum, c);
-  if (e.B > 96) out_flush(e, g, wr);
-  const u32 tot = e.total;
-  const double rt = e.rt;
-  e.total += p.inc;
-  e.rt = recip(e.total);
-  if (enc_code(e, cum, c, tot, rt)) enc_reduce(e, g, wr);
-  if ((i & p.pmask) == p.pmask && e.total > p.limit) {
-    tree_halve(tcol, e.total);
-    e.rt = recip(e.total);
-  }
-}
-
 // Encoder::finish (encoder.rs:40-46) when fin (8 x left_shift), then the last partial dword;
 // returns the stream length
 static __device__ __forceinline__ u32 enc_finish(AEnc& e, const AOut& g, bool wr, bool fin) {
@@ -353,202 +333,222 @@ static __device__ __forceinline__ u32 enc_finish(AEnc& e, const AOut& g, bool wr
   return e.wpos + rb - g.a;
 }
 
-// any of the 16 symbols of a tile outside the alphabet
-static __device__ __forceinline__ bool tile_bad(const u32x4& v, u32 n) {
-  const u32 w[4] = {v.x, v.y, v.z, v.w};
-  bool bad = false;
+// ---- the two-wave encoder ----
+// The adaptive model does not depend on the coder.  Wave 0 of a workgroup (the model wave)
+// walks and updates the 64 trees and hands (cum, c, total) per symbol to wave 1 (the coder
+// wave) through an LDS FIFO of two 8-symbol halves: while the model fills one half, the coder
+// codes the other, and one barrier per 8 symbols swaps them.  Tree + FIFO = 40 KiB, so 4
+// workgroups (8 waves) share a CU and each SIMD issues for 2 waves, at ~2.5 instead of ~5
+// cycles per VALU instruction (tools/ubench_issue.hip).
+#define EWG 128
+#define FIFO_SYMS 8
+#define FIFO_OFF TREE_BYTES                  // 32640: 8-B aligned, right after the tree
+#define FIFO_BYTES (2 * FIFO_SYMS * 64 * 8)  // 8 KiB
+// entry (half h, symbol j, lane L): (cum | c << 16, total | bad << 31); a wave's 64 entries are
+// one contiguous 512-B run (conflict-free ds_write_b64 / ds_read_b64)
+#define FIFO_AT(h, j, lane) (FIFO_OFF + ((((h) * FIFO_SYMS + (j)) * 64 + (lane)) << 3))
+
+typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 l_u32x2;
+
+static __device__ __forceinline__ u32x2 fifo_get(u32 a) { return *(const l_u32x2*)(uintptr_t)a; }
+
+// the 16 stream symbols [16 g, 16 g + 16) of a lane (its stream starts at byte mis of block 0)
+// as 4 words, from its 16-B blocks g and g + 1: a dword shift by mis >> 2 (two mask stages,
+// m0 / m1 = its bits as 0 / ~0), then a byte funnel by mis & 3
+static __device__ __forceinline__ void funnel4(u32 (&w)[4], const u32x4& b0, const u32x4& b1,
+                                               u32 m0, u32 m1, u32 mis) {
+  const u32 v[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  u32 v1[7], v2[5];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) bad |= ((w[j >> 2] >> (8 * (j & 3))) & 255u) >= n;
-  return bad;
-}
-
-// the per-lane geometry and state of the encoder kernel
-struct EncLane {
-  AEnc e;
-  AOut g;
-  bool wr, done;
-  u32 hd, nt, tl, nblk, col, k;
-  u64 cap;
-  const u32x4* tp;
-  uint16_t* tcol;
-};
-
-// lanes with all their tiles coded: the tail symbols (per lane, slow) and Encoder::finish
-static __device__ __forceinline__ void enc_lane_end(EncLane& L, l_char* tb, const u32x4& cur, us2 incp,
-                                    const AdaptParams& p, u32 t, u64* out_len, u32* flags) {
-  for (u32 j = 0; j < L.tl && !L.e.err; ++j) {
-    const u32 s = byte_at(cur, j);
-    if (s >= p.n)
-      L.e.err = RC_F_BAD_SYMBOL;  // the reference panics (sample_impl.rs:19)
-    else
-      enc_slow_sym(L.e, L.g, L.wr, tb, L.tcol, L.col, s, incp, p, L.hd + 16 * t + j);
-  }
-  const u32 len = enc_finish(L.e, L.g, L.wr, L.e.err == 0);
-  out_len[L.k] = len;
-  flags[L.k] = L.e.err ? L.e.err : ((u64)len > L.cap ? RC_F_CAPACITY : 0u);
-  L.done = true;
-  L.wr = false;
-}
-
-// The tile loop: T rounds of 16 symbols, every lane at tile t of its own input.  A lane whose
-// tiles run out finishes inside the loop and then runs on dummy input with its writes off.
-// UNI: all lanes share the head length, so the period's halving checks fall on the same
-// symbol in every lane (a scalar test).
-template <bool UNI>
-static __device__ __forceinline__ void enc_tiles(EncLane& L, l_char* tb, us2 incp, const AdaptParams& p, u32 T,
-                                 u32 hd_u, u64* out_len, u32* flags) {
-  auto blk = [&](u32 t) -> u32x4 {
-    return gload16(!L.done && t < L.nblk ? L.tp + t : &g_zero16);
-  };
-  u32x4 cur = blk(0), nxt = blk(1);
-  ESym q;
-  esym_prep(q, cur.x & 255u, L.col);
-  esym_load(q, tb);
-  for (u32 t = 0; t < T; ++t) {
-    const u32x4 pend = blk(t + 2);
-    if (__any((int)(!L.done && t == L.nt))) {
-      if (!L.done && t == L.nt) enc_lane_end(L, tb, cur, incp, p, t, out_len, flags);
-    }
-    // a tile with a symbol outside the alphabet: that lane codes up to it, slowly, and stops
-    if (p.n < 256) {
-      const bool bad = !L.done && tile_bad(cur, p.n);
-      if (__any((int)bad)) {
-        if (bad) {
-          for (u32 j = 0; j < 16 && !L.e.err; ++j) {
-            const u32 s = byte_at(cur, j);
-            if (s >= p.n)
-              L.e.err = RC_F_BAD_SYMBOL;
-            else
-              enc_slow_sym(L.e, L.g, L.wr, tb, L.tcol, L.col, s, incp, p, L.hd + 16 * t + j);
-          }
-          out_len[L.k] = enc_finish(L.e, L.g, L.wr, false);
-          flags[L.k] = L.e.err;
-          L.done = true;
-          L.wr = false;
-        }
-      }
-    }
-    const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
-    // symbol index of the tile's first symbol: scalar when UNI; else the per-lane offset of
-    // the first halving check inside the tile, d = (pmask - i0) & pmask
-    const u32 i0 = hd_u + 16 * t;
-    const u32 d = (p.pmask - (L.hd + 16 * t)) & p.pmask;
+  for (int i = 0; i < 7; ++i) v1[i] = msel(m0, v[i + 1], v[i]);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      u32 cum, c;
-      esym_code(q, tb, L.e.total, incp, cum, c);
-      const u32 tot = L.e.total;
-      const double rt = L.e.rt;
-      L.e.total += p.inc;
-      // the period's halving check after symbol i (adapt_update), before the next reads
-      bool at;
-      if (UNI)
-        at = ((i0 + j) & p.pmask) == p.pmask;
-      else
-        at = ((u32)j & p.pmask) == d;
-      if (!UNI || at) {
-        const bool h = !L.done && at && L.e.total > p.limit;
-        if (__builtin_expect(__any((int)h), 0)) {
-          if (h) tree_halve(L.tcol, L.e.total);
-        }
-      }
-      L.e.rt = recip(L.e.total);
-      const u32 sn = j < 15 ? (w[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 255u : nxt.x & 255u;
-      ESym qn;
-      esym_prep(qn, sn, L.col);
-      esym_load(qn, tb);
-      const bool rare = enc_code(L.e, cum, c, tot, rt);
-      if (__builtin_expect(__any((int)rare), 0)) {
-        if (rare) enc_reduce(L.e, L.g, L.wr);
-      }
-      if ((j & 3) == 3) out_flush(L.e, L.g, L.wr);
-      q = qn;
-    }
-    cur = nxt;
-    nxt = pend;
-  }
-  if (!L.done) enc_lane_end(L, tb, cur, incp, p, T, out_len, flags);
+  for (int i = 0; i < 5; ++i) v2[i] = msel(m1, v1[i + 2], v1[i]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = __builtin_amdgcn_alignbyte(v2[k + 1], v2[k], mis);
 }
 
-__global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_encode_adaptive(
-    AdaptParams p, const uint8_t* __restrict__ syms, const u64* __restrict__ sym_off,
-    u32 n_chunks, uint8_t* __restrict__ out, const u64* __restrict__ out_off,
-    u64* __restrict__ out_len, u32* __restrict__ flags) {
-  extern __shared__ uint16_t s_tree[];
+// The model wave's step t: symbols i = 8 t + j of every lane into FIFO half H.  All lanes are at
+// the same symbol index, so the period's halving check is a scalar test.  The next symbol's
+// tree reads are issued while the current one finishes, after the halving check.
+template <int H>
+static __device__ __forceinline__ void model_step(ESym& q, u32& total, const u32 (&w)[2],
+                                                  u32 wn, u32 t, uint16_t* tcol, l_char* tb,
+                                                  u32 col, u32 lane, us2 incp,
+                                                  const AdaptParams& p) {
+#pragma unroll
+  for (int j = 0; j < FIFO_SYMS; ++j) {
+    u32 cum, c;
+    const u32 s = q.s;
+    esym_code(q, tb, total, incp, cum, c);
+    const u32 tot = total;
+    total += p.inc;
+    if (((8u * t + j) & p.pmask) == p.pmask) {  // adapt_update's halving check
+      const bool h = total > p.limit;
+      if (__builtin_expect(__any((int)h), 0)) {
+        if (h) tree_halve(tcol, total);
+      }
+    }
+    const u32 sn = j < 7 ? (w[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 255u : wn & 255u;
+    ESym qn;
+    esym_prep(qn, sn, col);
+    esym_load(qn, tb);
+    // bit 31: a symbol outside the alphabet (the reference panics, sample_impl.rs:19), where
+    // the coder stops; c >= 1 keeps entries codable for lanes past their chunk's end
+    const u32 e1 = ((p.n - 1u - s) & 0x80000000u) | tot;
+    *(l_u32x2*)(uintptr_t)FIFO_AT(H, j, lane) = (u32x2){cum | (max(c, 1u) << 16), e1};
+    q = qn;
+  }
+}
+
+static __device__ __forceinline__ void model_wave(const AdaptParams& p, const uint8_t* sp, u64 n,
+                                                  bool live, u32 lane, u32 T,
+                                                  uint16_t* s_tree) {
   l_char* tb = (l_char*)s_tree;
-  const u32 lane = threadIdx.x;
-  EncLane L;
-  L.k = blockIdx.x * AWG + lane;
-  const bool live = L.k < n_chunks;
-  RC_VGPR_FLOOR_128();
-  u64 n = 0;
-  L.cap = 0;
-  const uint8_t* sp = syms;
-  uint8_t* lo = out;
-  if (live) {
-    const u64 a = sym_off[L.k], b = out_off[L.k];
-    n = sym_off[L.k + 1] - a;
-    sp = syms + a;
-    lo = out + b;
-    L.cap = out_off[L.k + 1] - b;
-  }
-  // lane L's u16 at byte 4 (L mod 32) + 2 (L div 32) of each row: a ds_read_u16 / ds_write_b16
-  // serves lanes 0-31 and 32-63 as separate groups, and within a group every lane has its own
-  // bank (lane pairs sharing a dword conflicted 2-way whenever they read different rows)
-  L.col = ((lane & 31u) << 2) | ((lane >> 5) << 1);
-  L.tcol = s_tree + (L.col >> 1);
-  tree_init(L.tcol, p.n);
+  const u32 col = ((lane & 31u) << 2) | ((lane >> 5) << 1);
+  uint16_t* tcol = s_tree + (col >> 1);
+  tree_init(tcol, p.n);
   const us2 incp = {(unsigned short)p.inc, (unsigned short)p.inc};
+  u32 total = p.n;
+  const u32 mis = (u32)(uintptr_t)sp & 15u;
+  const bool has = live && n > 0;
+  const u32x4* bp = (const u32x4*)(sp - mis);
+  const u32 blast = has ? (u32)((mis + n - 1) >> 4) : 0u;  // last block holding a symbol
+  auto blk = [&](u32 u) -> u32x4 { return gload16(has ? bp + min(u, blast) : &g_zero16); };
+  const u32 m0 = 0u - ((mis >> 2) & 1u), m1 = 0u - ((mis >> 3) & 1u);
+  u32x4 B1 = blk(1), B2 = blk(2);
+  u32 nw[4];
+  funnel4(nw, blk(0), B1, m0, m1, mis);  // group 0
+  ESym q;
+  esym_prep(q, nw[0] & 255u, col);
+  esym_load(q, tb);
+  // one 16-symbol group (two steps) per iteration, a barrier after each step: T + 1 barriers
+  // in all, as in the coder wave
+  for (u32 t = 0; t <= T; t += 2) {
+    u32 cw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cw[k] = nw[k];
+    if (t < T) {
+      funnel4(nw, B1, B2, m0, m1, mis);  // the next group (its first symbol is looked ahead)
+      B1 = B2;
+      B2 = blk((t >> 1) + 3);
+      const u32 wa[2] = {cw[0], cw[1]};
+      model_step<0>(q, total, wa, cw[2], t, tcol, tb, col, lane, incp, p);
+    }
+    __syncthreads();
+    if (t + 1 <= T) {
+      if (t + 1 < T) {
+        const u32 wb[2] = {cw[2], cw[3]};
+        model_step<1>(q, total, wb, nw[0], t + 1, tcol, tb, col, lane, incp, p);
+      }
+      __syncthreads();
+    }
+  }
+}
 
-  AEnc& e = L.e;
+// The coder wave's step: FIFO half H, symbols i0 .. i0 + 7 of every lane.  A lane whose chunk
+// ends inside the step, or meets a symbol outside the alphabet, first finishes per lane and then
+// runs along with its writes off.
+template <int H>
+static __device__ __forceinline__ void coder_step(AEnc& e, const AOut& g, bool& wr, bool& done,
+                                                  u32 i0, u64 n, u64 cap, u32 lane, u32 k,
+                                                  const AdaptParams& p, u64* out_len,
+                                                  u32* flags) {
+  bool slow = !done && (u64)i0 + FIFO_SYMS > n;
+  if (p.n < 256) {  // an entry of this chunk flagged bad in this step
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < FIFO_SYMS; ++j)
+      bad = bad || ((u64)i0 + j < n && (fifo_get(FIFO_AT(H, j, lane)).y >> 31));
+    slow = slow || (!done && bad);
+  }
+  if (__builtin_expect(__any((int)slow), 0)) {
+    if (slow) {
+      for (u32 j = 0; j < FIFO_SYMS && (u64)i0 + j < n; ++j) {
+        const u32x2 en = fifo_get(FIFO_AT(H, j, lane));
+        if (en.y >> 31) {
+          e.err = RC_F_BAD_SYMBOL;
+          break;
+        }
+        if (e.B > 96) out_flush(e, g, wr);
+        const u32 tot = en.y & 0xFFFFu;
+        if (enc_code(e, en.x & 0xFFFFu, en.x >> 16, tot, recip(tot))) enc_reduce(e, g, wr);
+      }
+      const u32 len = enc_finish(e, g, wr, e.err == 0);
+      out_len[k] = len;
+      flags[k] = e.err ? e.err : ((u64)len > cap ? RC_F_CAPACITY : 0u);
+      done = true;
+      wr = false;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < FIFO_SYMS; ++j) {
+    const u32x2 en = fifo_get(FIFO_AT(H, j, lane));
+    const u32 tot = en.y & 0xFFFFu;
+    const bool rare = enc_code(e, en.x & 0xFFFFu, en.x >> 16, tot, recip(tot));
+    if (__builtin_expect(__any((int)rare), 0)) {
+      if (rare) enc_reduce(e, g, wr);
+    }
+    if ((j & 3) == 3) out_flush(e, g, wr);
+  }
+}
+
+static __device__ __forceinline__ void coder_wave(const AdaptParams& p, u64 n, u64 cap,
+                                                  uint8_t* lo, bool live, u32 lane, u32 k,
+                                                  u32 T, u64* out_len, u32* flags) {
+  AEnc e;
   e.low = 0;
   e.range = ~0ull;  // RangeCoder::default (range_coder.rs:13-20)
   e.W0 = e.W1 = e.W2 = e.W3 = 0;
   e.wpos = 0;
-  e.total = p.n;
-  e.rt = recip(p.n);
   e.err = 0;
-  L.g.o = (uint8_t*)((uintptr_t)lo & ~(uintptr_t)3);
-  L.g.a = (u32)((uintptr_t)lo & 3);
-  L.g.end = L.g.a + (u32)min(L.cap, (u64)(0xFFFFFF00u - L.g.a));
-  e.B = 8 * L.g.a;
-  L.wr = live;
-  L.done = !live;
-
-  // symbols [0, hd) until the input is 16-B aligned, then nt 16-symbol tiles, then tl symbols
-  const u32 mis = (u32)(uintptr_t)sp & 15u;
-  L.hd = live ? (u32)min((u64)((16u - mis) & 15u), n) : 0u;
-  L.nt = live ? (u32)((n - L.hd) >> 4) : 0u;
-  L.tl = live ? (u32)((n - L.hd) & 15u) : 0u;
-  L.nblk = L.nt + (L.tl ? 1u : 0u);
-  L.tp = (const u32x4*)(sp + L.hd);
-
-  if (__any((int)(L.hd > 0))) {  // head (per lane, slow)
-    const u32x4 hb = gload16(L.hd > 0 ? (const u32x4*)(sp - mis) : &g_zero16);
-    for (u32 j = 0; __any((int)(j < L.hd && !e.err)); ++j) {
-      if (j < L.hd && !e.err) {
-        const u32 s = byte_at(hb, mis + j);
-        if (s >= p.n)
-          e.err = RC_F_BAD_SYMBOL;  // the reference panics (sample_impl.rs:19)
-        else
-          enc_slow_sym(e, L.g, L.wr, tb, L.tcol, L.col, s, incp, p, j);
-      }
-    }
-    if (live && e.err) {
-      out_len[L.k] = enc_finish(e, L.g, L.wr, false);
-      flags[L.k] = e.err;
-      L.done = true;
-      L.wr = false;
+  AOut g;
+  g.o = (uint8_t*)((uintptr_t)lo & ~(uintptr_t)3);
+  g.a = (u32)((uintptr_t)lo & 3);
+  g.end = g.a + (u32)min(cap, (u64)(0xFFFFFF00u - g.a));
+  e.B = 8 * g.a;
+  bool wr = live, done = !live;
+  for (u32 t = 0; t <= T; t += 2) {  // the model wave's barrier sequence, one step behind
+    if (t >= 1) coder_step<1>(e, g, wr, done, 8 * (t - 1), n, cap, lane, k, p, out_len, flags);
+    __syncthreads();
+    if (t + 1 <= T) {
+      coder_step<0>(e, g, wr, done, 8 * t, n, cap, lane, k, p, out_len, flags);
+      __syncthreads();
     }
   }
-  out_flush(e, L.g, L.wr);  // B <= 31 for the tile loop
+  if (!done) {  // chunks ending on a step boundary: Encoder::finish
+    const u32 len = enc_finish(e, g, wr, true);
+    out_len[k] = len;
+    flags[k] = (u64)len > cap ? RC_F_CAPACITY : 0u;
+  }
+}
 
-  const u32 T = wave_max(L.done ? 0u : L.nt);
-  const u32 hmin = wave_min(L.done ? 16u : L.hd), hmax = wave_max(L.done ? 0u : L.hd);
-  if (hmin >= hmax)
-    enc_tiles<true>(L, tb, incp, p, T, hmax, out_len, flags);
+__global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_encode_adaptive(
+    AdaptParams p, const uint8_t* __restrict__ syms, const u64* __restrict__ sym_off,
+    u32 n_chunks, uint8_t* __restrict__ out, const u64* __restrict__ out_off,
+    u64* __restrict__ out_len, u32* __restrict__ flags) {
+  extern __shared__ uint16_t s_tree[];
+  const u32 lane = threadIdx.x & 63u;
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 k = blockIdx.x * 64 + lane;
+  const bool live = k < n_chunks;
+  RC_VGPR_FLOOR_128();
+  u64 n = 0, cap = 0;
+  const uint8_t* sp = syms;
+  uint8_t* lo = out;
+  if (live) {
+    const u64 a = sym_off[k], b = out_off[k];
+    n = sym_off[k + 1] - a;
+    sp = syms + a;
+    lo = out + b;
+    cap = out_off[k + 1] - b;
+  }
+  // 8-symbol steps: the same count in both waves (they hold the same 64 chunks)
+  const u32 T = __builtin_amdgcn_readfirstlane(wave_max(live ? (u32)((n + 7) >> 3) : 0u));
+  if (wave == 0)
+    model_wave(p, sp, n, live, lane, T, s_tree);
   else
-    enc_tiles<false>(L, tb, incp, p, T, 0, out_len, flags);
+    coder_wave(p, n, cap, lo, live, lane, k, T, out_len, flags);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -923,9 +923,9 @@ hipError_t rc_adaptive_encode_launch(hipStream_t stream, const AdaptParams& p,
                                      const uint8_t* syms, const u64* sym_off, u32 n_chunks,
                                      uint8_t* out, const u64* out_off, u64* out_len,
                                      u32* flags) {
-  hipLaunchKernelGGL(k_encode_adaptive, dim3((n_chunks + AWG - 1) / AWG), dim3(AWG),
-                     TREE_BYTES, stream, p, syms, sym_off, n_chunks, out, out_off, out_len,
-                     flags);
+  hipLaunchKernelGGL(k_encode_adaptive, dim3((n_chunks + 63) / 64), dim3(EWG),
+                     TREE_BYTES + FIFO_BYTES, stream, p, syms, sym_off, n_chunks, out, out_off,
+                     out_len, flags);
   return hipGetLastError();
 }
 
