@@ -20,6 +20,7 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 #define RC_VGPR_FLOOR_48() asm volatile("; vgpr floor 48" ::: "v47")
 #define RC_VGPR_FLOOR_64() asm volatile("; vgpr floor 64" ::: "v63")
 #define RC_VGPR_FLOOR_96() asm volatile("; vgpr floor 96" ::: "v95")
+#define RC_VGPR_FLOOR_80() asm volatile("; vgpr floor 80" ::: "v79")
 #define RC_VGPR_FLOOR_112() asm volatile("; vgpr floor 112" ::: "v111")
 #define RC_VGPR_FLOOR_128() asm volatile("; vgpr floor 128" ::: "v127")
 #define RC_VGPR_FLOOR_144() asm volatile("; vgpr floor 144" ::: "v143")
@@ -35,6 +36,15 @@ static __device__ __forceinline__ u64 sub64(u64 a, u64 b) {
   asm("v_sub_co_u32_e64 %0, %2, %3, %4\n\tv_subb_co_u32_e64 %1, %2, %5, %6, %2"
       : "=&v"(lo), "=&v"(hi), "=&s"(c)
       : "v"((u32)a), "v"((u32)b), "v"(hi32(a)), "v"(hi32(b)));
+  return ((u64)hi << 32) | lo;
+}
+// the same with a given as two halves (no register pair needed for it)
+static __device__ __forceinline__ u64 sub64(u32 alo, u32 ahi, u64 b) {
+  u32 lo, hi;
+  u64 c;
+  asm("v_sub_co_u32_e64 %0, %2, %3, %4\n\tv_subb_co_u32_e64 %1, %2, %5, %6, %2"
+      : "=&v"(lo), "=&v"(hi), "=&s"(c)
+      : "v"(alo), "v"((u32)b), "v"(ahi), "v"(hi32(b)));
   return ((u64)hi << 32) | lo;
 }
 

@@ -24,8 +24,10 @@
 #define WG 256
 #define WAVES (WG / 64)
 #define ENC_RING 32          // dwords per lane in the encoder's output ring (128 B)
-#define DEC_RING 32          // dwords per lane in the decoder's input ring (128 B)
-#define DEC_RING_ALLOC 36    // + 4 mirror slots so a 5-dword read never wraps
+#define DEC_RING 16          // dwords per lane in the decoder's input ring (64 B)
+#define DEC_RING_ALLOC 20    // + 4 mirror slots so a 5-dword read never wraps
+#define DEC_PF 2             // 16-B blocks per ring refill (32 B, one 16-symbol phase ahead)
+#define DEC_LD 4             // 16-B blocks per global load burst (64 B: two refills)
 #define LUT_BITS 12
 #define LUT_MAX_ENTRIES (1u << LUT_BITS)
 
@@ -55,10 +57,19 @@ static __device__ __forceinline__ u64 range_par_total(u64 range, const ModelArgs
 }
 
 // r * v for the coder's products (range_coder.rs:65, :70).  SM (256 <= total <= 2^16): r < 2^56
-// and v <= 2^16, so the high half is a 24-bit multiply.
+// and v <= 2^16, so the high half is a 24-bit multiply.  SM is written out as two
+// instructions, lo(r)*v as a 64-bit product plus a 24-bit mad into its high half: from the C
+// form the compiler re-derives the low half with an extra v_mul_lo_u32 and zeroes the mad's
+// addend with two moves (three extra VALU per product).
 template <int SM>
 static __device__ __forceinline__ u64 mul_rv(u64 r, u32 v) {
-  if (SM) return (u64)(u32)r * v + ((u64)__umul24(hi32(r), v) << 32);
+  if (SM) {
+    u64 p, c;
+    u32 h;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(c) : "v"((u32)r), "v"(v));
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(r)), "v"(v), "v"(hi32(p)));
+    return ((u64)h << 32) | (u32)p;
+  }
   return r * (u64)v;
 }
 
@@ -448,36 +459,42 @@ typedef __attribute__((address_space(3))) u32 l_u32;
 
 struct Dec {
   u64 low, range;  // RangeCoder (decoder.rs:6-12)
-  u64 x;           // Decoder::data - lower_bound (mod 2^64): all find_index needs (sample_impl.rs:29)
+  // Decoder::data - lower_bound (mod 2^64): all find_index needs (sample_impl.rs:29).  Kept as
+  // two 32-bit halves: as a u64 it must sit in an even-aligned VGPR pair, which costs a move
+  // per symbol when its new halves are produced in other registers.
+  u32 xlo, xhi;
+  __device__ __forceinline__ u64 x() const { return ((u64)xhi << 32) | xlo; }
+  __device__ __forceinline__ void set_x(u64 v) { xlo = (u32)v; xhi = hi32(v); }
   u32 cpos;   // bytes consumed, relative to the 16-B aligned base of the code stream
   u32 fill;   // bytes staged into the ring, same origin
   u32 lim;    // cpos > lim: more bytes consumed than the stream holds
   u32 err;
-  u32 pend_ok;           // a 64-B load is in flight in pend[]
+  u32 pend_ok;           // 32-B refills still held in pend[] (a load burst gives DEC_LD / DEC_PF)
   l_u32* ring;           // this lane's ring column: dword j at ring[j * 64] (LDS pointer)
   const uint4* gbase;    // 16-B aligned base of the stream
   u32 gnext;             // next 16-B block (index from gbase)
   u32 glast;             // last block holding a byte of this chunk (fetch clamp)
-  uint4 pend[4];
+  uint4 pend[DEC_LD];
 };
 
 static __device__ __forceinline__ void dec_issue(Dec& d) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < DEC_LD; ++q) {
     // 32-bit block index clamp (v_min_u32): a 64-bit pointer compare would select on VCC
     const uint4* p = d.gbase + min(d.gnext + q, d.glast);
     const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;  // global, not flat
     d.pend[q] = make_uint4(v.x, v.y, v.z, v.w);
   }
-  d.gnext += 4;
-  d.pend_ok = 1;
+  d.gnext += DEC_LD;
+  d.pend_ok = DEC_LD / DEC_PF;
 }
 
+// move the next DEC_PF pending blocks into the ring (pend[0..DEC_PF) hold them)
 static __device__ __forceinline__ void dec_commit(Dec& d) {
   const u32 j = (d.fill >> 2) & (DEC_RING - 1);
   l_u32* rp = d.ring + j * 64;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < DEC_PF; ++q) {
     rp[(4 * q + 0) * 64] = d.pend[q].x;
     rp[(4 * q + 1) * 64] = d.pend[q].y;
     rp[(4 * q + 2) * 64] = d.pend[q].z;
@@ -489,14 +506,18 @@ static __device__ __forceinline__ void dec_commit(Dec& d) {
     rp[(DEC_RING + 2) * 64] = d.pend[0].z;
     rp[(DEC_RING + 3) * 64] = d.pend[0].w;
   }
-  d.fill += 64;
-  d.pend_ok = 0;
+#pragma unroll
+  for (int q = 0; q + DEC_PF < DEC_LD; ++q) d.pend[q] = d.pend[q + DEC_PF];
+  d.fill += 16 * DEC_PF;
+  d.pend_ok -= 1;
 }
 
 // phase boundary: commit the pending load, issue the next one if the ring has room
+// (the ring has room for a refill once at most 4 * DEC_RING - 16 * DEC_PF bytes are unread;
+// a 64-B load burst feeds two refills, so every lane's global reads are whole 64-B segments)
 static __device__ __forceinline__ void dec_phase(Dec& d) {
-  if (d.pend_ok) dec_commit(d);
-  if ((int)(d.fill - d.cpos) <= 56) dec_issue(d);
+  if (d.pend_ok && (int)(d.fill - d.cpos) <= 4 * DEC_RING - 16 * DEC_PF) dec_commit(d);
+  if (!d.pend_ok) dec_issue(d);
 }
 
 // a lane about to read past the staged bytes: commit / load synchronously (rare)
@@ -531,7 +552,7 @@ static __device__ __forceinline__ void dec_rare(Dec& d, u32 need) {
   dec_sync(d, m + need);
   for (u32 j = 0; j < m; ++j, ++d.cpos) {
     const u32 w = d.ring[((d.cpos >> 2) & (DEC_RING - 1)) * 64];
-    d.x = (d.x << 8) | ((w >> (8 * (d.cpos & 3))) & 255u);
+    d.set_x((d.x() << 8) | ((w >> (8 * (d.cpos & 3))) & 255u));
   }
 }
 
@@ -608,7 +629,6 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   const l_u32* rp = d.ring + ((d.cpos >> 2) & (DEC_RING - 1)) * 64;
   const u32 D0 = rp[0], D1 = rp[64];
   const u32 D2 = SM ? 0u : rp[128];
-  const u64 x = d.x;
   const u64 r = range_par_total<DIV>(d.range, m);
   // hint q ~ x / r ~ x * total / range from the top 32 bits of x and range.  Direct tables
   // (total <= 2048) take the high halves as they are: range >= 2^48, so the relative error is
@@ -616,11 +636,11 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   // tables (totals up to 2^32) first shift both by clz(range), for a relative error ~2^-22.
   float X, R;
   if (LUT) {
-    X = cvt_f32(hi32(x));
+    X = cvt_f32(d.xhi);
     R = cvt_f32(hi32(d.range));
   } else {
     const u32 e = (u32)__builtin_clz(hi32(d.range));
-    X = cvt_f32(hi32(x << e));
+    X = cvt_f32(hi32(d.x() << e));
     R = cvt_f32(hi32(d.range << e));
   }
   // The table index is masked, not clamped: the tables are padded to a power of two with valid
@@ -648,17 +668,17 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   // exact verification r*cum[s] <= x < r*cum[s+1] as ONE unsigned test: A + B <= range < 2^64,
   // so when A > x the wrapped difference x - A is >= 2^64 - A > B.  The hint is rarely off.
   // (At s = n - 1 the test fails only on corrupt input, x >= r * total: dec_fix keeps s = n-1.)
-  u64 dx = sub64(x, A);
+  u64 dx = sub64(d.xlo, d.xhi, A);
   if (__builtin_expect(__any((int)(dx >= B)), 0)) {
     if (dx >= B) {
-      dec_fix(s, t, A, B, x, r, s_tab, m.n);
+      dec_fix(s, t, A, B, d.x(), r, s_tab, m.n);
       // the tables only hold symbols with c > 0, so c == 0 can only come from dec_fix: corrupt
       // input (the reference loops forever); an over-read, if any, came first
       if (t.y == 0) {
         d.err = d.err ? d.err : (d.cpos > d.lim ? RC_F_TRUNCATED : RC_F_CORRUPT);
         B = r;
       }
-      dx = sub64(x, A);
+      dx = sub64(d.xlo, d.xhi, A);
     }
   }
   // param_update (range_coder.rs:53-92)
@@ -673,14 +693,20 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   // data' = data << k8 | k settled bytes and low' = (low + A) << k8, so x' = ((x - A) << k8) |
   // those bytes (shift_left_buffer, decoder.rs:31-35): the high half of dx << k8, and the high
   // half of (dx_lo : next 4 code bytes) << k8 (alignbyte uses cpos & 3 only)
-  const u32 w0 = __builtin_bswap32(__builtin_amdgcn_alignbyte(D1, D0, d.cpos));
-  if (SM) {  // k8 <= 24
-    const u32 xh = hi32(dx << k8);
-    const u32 xl = hi32((((u64)(u32)dx) << 32 | w0) << k8);
-    d.x = ((u64)xh << 32) | xl;
+  if (SM) {  // k8 = 8n <= 24
+    // xl = dx_lo << 8n | the n code bytes at cpos, first byte highest: ONE v_perm_b32 over
+    // {dx_lo, W} (W = the 4 code bytes at cpos, first byte in byte 0) whose selector is
+    // hi32(0x0706050400010203 << 8n): byte j takes dx_lo byte j - n (j >= n) or W byte
+    // n - 1 - j (j < n).  (No byte swap, no register pair to assemble.)
+    const u32 W = __builtin_amdgcn_alignbyte(D1, D0, d.cpos);
+    const u32 sel = hi32(0x0706050400010203ull << k8);
+    const u32 xl = __builtin_amdgcn_perm((u32)dx, W, sel);
+    d.xhi = hi32(dx << k8);
+    d.xlo = xl;
   } else {   // k8 <= 56
+    const u32 w0 = __builtin_bswap32(__builtin_amdgcn_alignbyte(D1, D0, d.cpos));
     const u64 b = ((u64)w0 << 32) | __builtin_bswap32(__builtin_amdgcn_alignbyte(D2, D1, d.cpos));
-    d.x = (dx << k8) | (k8 ? b >> (64 - k8) : 0ull);
+    d.set_x((dx << k8) | (k8 ? b >> (64 - k8) : 0ull));
   }
   u32 nbytes;  // k8 >> 3 as a plain shift (the compiler's v_bfe from the ffbh result costs more)
   asm("v_lshrrev_b32 %0, 3, %1" : "=v"(nbytes) : "v"(k8));
@@ -704,6 +730,20 @@ static __device__ __forceinline__ void dec_check4(Dec& d) {
   }
 }
 
+// 16 symbols into one 16-B block (byte j of word q = symbol 4q + j), with the ring checks
+template <int DIV, int SM, int LUT>
+static __device__ __forceinline__ uint4 dec_phase16(Dec& d, const ModelArgs& m,
+                                                    const uint2* s_tab, const u32* s_lut) {
+  u32 w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[q] = put_byte(w[q], dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut), j);
+    if (q < 3) dec_check4<SM>(d);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 template <int DIV, int SM, int LUT>
 __global__ __launch_bounds__(WG) void k_decode_static(
     ModelArgs m, const uint8_t* __restrict__ code, const u64* __restrict__ code_off,
@@ -722,7 +762,7 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   __syncthreads();
   const u32 k = blockIdx.x * WG + tid;
   if (k >= n_chunks) return;
-  RC_VGPR_FLOOR_112();
+  RC_VGPR_FLOOR_64();
   const u32 lane = tid & 63, wave = tid >> 6;
 
   const u64 c0 = code_off[k];
@@ -751,29 +791,49 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   d.lim = (u32)(clen < 0xFFFFFF00ull - a ? a + clen : 0xFFFFFF00ull);
   dec_issue(d);
   dec_commit(d);
+  dec_commit(d);
   dec_issue(d);
-  d.x = dec_read8_before(d);  // data - low with low = 0
+  d.set_x(dec_read8_before(d));  // data - low with low = 0
 
   u64 i = 0;
-  u64 head = (16 - ((uintptr_t)op & 15)) & 15;
+  // head: single symbols until the output is 64-B aligned
+  u64 head = (64 - ((uintptr_t)op & 63)) & 63;
   if (head > n) head = n;
   dec_check4<SM>(d);
   for (; i < head; ++i) {
     op[i] = (uint8_t)dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut);
     dec_check4<SM>(d);
   }
-  // body: 16-symbol phases: store decoded block, commit pending load, maybe issue the next
-  const u64 nph = (n - i) >> 4;
+  // body: 16-symbol phases (after each: commit a refill, maybe issue the next load burst).
+  // Decoded symbols leave in 64-B bursts per lane (4 phases, four back-to-back 16-B stores to
+  // one 64-B segment): HBM sees whole 64-B writes, not 16-B partial ones.
   uint4* ob = reinterpret_cast<uint4*>(op + i);
+  const u64 nbu = (n - i) >> 6;
+  for (u64 b = 0; b < nbu; ++b) {
+    // written out: the compiler declines to unroll a 64-symbol loop and would then index the
+    // blocks through scratch
+    const uint4 o0 = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
+    dec_phase(d);
+    dec_check4<SM>(d);
+    const uint4 o1 = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
+    dec_phase(d);
+    dec_check4<SM>(d);
+    const uint4 o2 = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
+    dec_phase(d);
+    dec_check4<SM>(d);
+    const uint4 o3 = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
+    dec_phase(d);
+    dec_check4<SM>(d);
+    ob[4 * b + 0] = o0;
+    ob[4 * b + 1] = o1;
+    ob[4 * b + 2] = o2;
+    ob[4 * b + 3] = o3;
+  }
+  i += nbu << 6;
+  ob += 4 * nbu;
+  const u64 nph = (n - i) >> 4;
   for (u64 b = 0; b < nph; ++b) {
-    u32 w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[q] = put_byte(w[q], dec_sym<DIV, SM, LUT>(d, m, s_tab, s_lut), j);
-      if (q < 3) dec_check4<SM>(d);
-    }
-    ob[b] = make_uint4(w[0], w[1], w[2], w[3]);
+    ob[b] = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
     dec_phase(d);
     dec_check4<SM>(d);
   }
