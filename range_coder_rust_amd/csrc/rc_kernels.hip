@@ -24,10 +24,25 @@
 #define WG 256
 #define WAVES (WG / 64)
 #define ENC_RING 32          // dwords per lane in the encoder's output ring (128 B)
+#ifndef DEC_RING
 #define DEC_RING 16          // dwords per lane in the decoder's input ring (64 B)
-#define DEC_RING_ALLOC 20    // + 4 mirror slots so a 5-dword read never wraps
+#endif
+#ifndef DEC_MIRROR
+#define DEC_MIRROR 2         // mirror slots past the ring, so a 3-dword read never wraps
+#endif
+#define DEC_RING_ALLOC (DEC_RING + DEC_MIRROR)
+#ifndef DEC_PF
 #define DEC_PF 2             // 16-B blocks per ring refill (32 B, one 16-symbol phase ahead)
+#endif
+#ifndef DEC_LD
 #define DEC_LD 4             // 16-B blocks per global load burst (64 B: two refills)
+#endif
+#ifndef DEC_OUT_BURST
+#define DEC_OUT_BURST 4      // 16-B symbol blocks per lane per output burst (4: 64 B)
+#endif
+#ifndef DEC_TAB_LDS
+#define DEC_TAB_LDS 1        // direct-LUT decoders: keep the (cum, c) table in LDS too
+#endif
 #define LUT_BITS 12
 #define LUT_MAX_ENTRIES (1u << LUT_BITS)
 
@@ -503,8 +518,8 @@ static __device__ __forceinline__ void dec_commit(Dec& d) {
   if (j == 0) {  // mirror slots
     rp[DEC_RING * 64] = d.pend[0].x;
     rp[(DEC_RING + 1) * 64] = d.pend[0].y;
-    rp[(DEC_RING + 2) * 64] = d.pend[0].z;
-    rp[(DEC_RING + 3) * 64] = d.pend[0].w;
+    if (DEC_MIRROR > 2) rp[(DEC_RING + 2) * 64] = d.pend[0].z;
+    if (DEC_MIRROR > 3) rp[(DEC_RING + 3) * 64] = d.pend[0].w;
   }
 #pragma unroll
   for (int q = 0; q + DEC_PF < DEC_LD; ++q) d.pend[q] = d.pend[q + DEC_PF];
@@ -755,9 +770,11 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   extern __shared__ u32 s_dyn[];
   u32* s_lut = s_dyn;
   const u32 lut_words = (m.lut_max + 2) & ~1u;  // 8-B aligned s_tab
-  uint2* s_tab = reinterpret_cast<uint2*>(s_dyn + lut_words);
+  // (direct tables hold (cum, c) themselves; then only the rare exact fix-up reads the table)
+  constexpr bool tab_lds = !LUT || DEC_TAB_LDS;
+  const uint2* s_tab = tab_lds ? reinterpret_cast<const uint2*>(s_dyn + lut_words) : m.tab;
   const u32 tid = threadIdx.x;
-  s_tab[tid] = m.tab[tid];
+  if (tab_lds) reinterpret_cast<uint2*>(s_dyn + lut_words)[tid] = m.tab[tid];
   for (u32 j = tid; j <= m.lut_max; j += WG) s_lut[j] = m.lut[j];
   __syncthreads();
   const u32 k = blockIdx.x * WG + tid;
@@ -783,21 +800,26 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   d.fill = 0;
   d.pend_ok = 0;
   // the ring as a plain LDS address (s_dyn is at 0), one register: no per-access base math
-  d.ring = (l_u32*)(uintptr_t)((lut_words + 512) * 4) + wave * DEC_RING_ALLOC * 64 + lane;
+  d.ring = (l_u32*)(uintptr_t)((lut_words + (tab_lds ? 512 : 0)) * 4) +
+           wave * DEC_RING_ALLOC * 64 + lane;
   d.gbase = reinterpret_cast<const uint4*>(cp - a);
   d.gnext = 0;
   d.glast = (u32)((a + clen - 1) >> 4);
   d.cpos = a + 8;  // Decoder::new primes 8 bytes (decoder.rs:21)
   d.lim = (u32)(clen < 0xFFFFFF00ull - a ? a + clen : 0xFFFFFF00ull);
-  dec_issue(d);
-  dec_commit(d);
-  dec_commit(d);
-  dec_issue(d);
+  // fill the whole ring, and have the next load burst in flight
+#pragma unroll
+  for (int h = 0; h < DEC_RING / (4 * DEC_PF); ++h) {
+    if (!d.pend_ok) dec_issue(d);
+    dec_commit(d);
+  }
+  if (!d.pend_ok) dec_issue(d);
   d.set_x(dec_read8_before(d));  // data - low with low = 0
 
   u64 i = 0;
   // head: single symbols until the output is 64-B aligned
-  u64 head = (64 - ((uintptr_t)op & 63)) & 63;
+  constexpr u32 OUT_ALIGN = 16 * DEC_OUT_BURST;  // (symbols before the first aligned burst)
+  u64 head = (OUT_ALIGN - ((uintptr_t)op & (OUT_ALIGN - 1))) & (OUT_ALIGN - 1);
   if (head > n) head = n;
   dec_check4<SM>(d);
   for (; i < head; ++i) {
@@ -808,29 +830,27 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   // Decoded symbols leave in 64-B bursts per lane (4 phases, four back-to-back 16-B stores to
   // one 64-B segment): HBM sees whole 64-B writes, not 16-B partial ones.
   uint4* ob = reinterpret_cast<uint4*>(op + i);
-  const u64 nbu = (n - i) >> 6;
+  const u64 nbu = DEC_OUT_BURST > 1 ? (n - i) / (16 * DEC_OUT_BURST) : 0;
   for (u64 b = 0; b < nbu; ++b) {
     // written out: the compiler declines to unroll a 64-symbol loop and would then index the
     // blocks through scratch
-    const uint4 o0 = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
-    dec_phase(d);
-    dec_check4<SM>(d);
-    const uint4 o1 = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
-    dec_phase(d);
-    dec_check4<SM>(d);
-    const uint4 o2 = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
-    dec_phase(d);
-    dec_check4<SM>(d);
-    const uint4 o3 = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
-    dec_phase(d);
-    dec_check4<SM>(d);
-    ob[4 * b + 0] = o0;
-    ob[4 * b + 1] = o1;
-    ob[4 * b + 2] = o2;
-    ob[4 * b + 3] = o3;
+#define RC_DEC_PHASE(o)                                          \
+  const uint4 o = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut); \
+  dec_phase(d);                                                  \
+  dec_check4<SM>(d);
+    RC_DEC_PHASE(o0) RC_DEC_PHASE(o1) RC_DEC_PHASE(o2) RC_DEC_PHASE(o3)
+    uint4* ob_b = ob + DEC_OUT_BURST * b;
+    if (DEC_OUT_BURST == 8) {
+      RC_DEC_PHASE(o4) RC_DEC_PHASE(o5) RC_DEC_PHASE(o6) RC_DEC_PHASE(o7)
+      ob_b[0] = o0; ob_b[1] = o1; ob_b[2] = o2; ob_b[3] = o3;
+      ob_b[4] = o4; ob_b[5] = o5; ob_b[6] = o6; ob_b[7] = o7;
+    } else {
+      ob_b[0] = o0; ob_b[1] = o1; ob_b[2] = o2; ob_b[3] = o3;
+    }
+#undef RC_DEC_PHASE
   }
-  i += nbu << 6;
-  ob += 4 * nbu;
+  i += nbu * 16 * DEC_OUT_BURST;
+  ob += DEC_OUT_BURST * nbu;
   const u64 nph = (n - i) >> 4;
   for (u64 b = 0; b < nph; ++b) {
     ob[b] = dec_phase16<DIV, SM, LUT>(d, m, s_tab, s_lut);
@@ -1239,7 +1259,8 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   const bool dl = m->args.direct != 0;
   // dynamic LDS of k_decode_static: LUT (8-B aligned), the (cum, c) table, the code rings
   const size_t lut_bytes = ((size_t)(m->args.lut_max + 2) & ~(size_t)1) * sizeof(u32) +
-                           256 * sizeof(uint2) + WAVES * DEC_RING_ALLOC * 64 * sizeof(u32);
+                           (!dl || DEC_TAB_LDS ? 256 * sizeof(uint2) : 0) +
+                           WAVES * DEC_RING_ALLOC * 64 * sizeof(u32);
 #ifdef RC_DEV_ONLY
   if (m->div != DIV_POW2 || !sm) return RC_E_ARG;
   if (dl) RC_DEC_LAUNCH(DIV_POW2, 1, 1); else RC_DEC_LAUNCH(DIV_POW2, 1, 0);
