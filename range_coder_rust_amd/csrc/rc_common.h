@@ -9,6 +9,7 @@
 typedef uint64_t u64;
 typedef uint32_t u32;
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+typedef u32 u32x3 __attribute__((ext_vector_type(3)));
 
 #define TOP16 (1ull << 48)  // range_coder.rs:24
 

@@ -59,6 +59,7 @@ struct ModelArgs {
   u32 lut_max;       // number of buckets - 1
   float ftotal;      // (float)total
   u32 direct;        // 1: lut[q] = s | cum << 8 | c << 20 for every q < total (total <= 2048)
+                     // 2: lut[4q..4q+3] = {cum, c, s, 0} (256 <= total <= 512)
 };
 
 
@@ -665,7 +666,12 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   const float rR = __builtin_amdgcn_rcpf(R);
   u32 s;
   uint2 t;
-  if (LUT) {  // direct table: candidate symbol and its (cum, c) in one LDS read at byte 4q
+  if (LUT == 2) {  // 16-B direct entries {cum, c, s}: one ds_read_b96 at byte 16q, no unpacking
+    const u32 q16 = cvt_u32_sat(X * ((16.0f * m.ftotal) * rR)) & (m.lut_max << 4);
+    const u32x3 ent = *(const __attribute__((address_space(3))) u32x3*)(uintptr_t)q16;
+    s = ent.z;
+    t = make_uint2(ent.x, ent.y);
+  } else if (LUT) {  // direct table: candidate symbol and its (cum, c) in one LDS read at byte 4q
     // the LUT is the kernel's first LDS object (address 0): q4 is its LDS byte address
     const u32 q4 = cvt_u32_sat(X * ((4.0f * m.ftotal) * rR)) & (m.lut_max << 2);
     const u32 ent = *(const __attribute__((address_space(3))) u32*)(uintptr_t)q4;
@@ -769,13 +775,14 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   // hint's byte offset with no base add; then the (cum, c) table and the code rings.
   extern __shared__ u32 s_dyn[];
   u32* s_lut = s_dyn;
-  const u32 lut_words = (m.lut_max + 2) & ~1u;  // 8-B aligned s_tab
+  const u32 lut_n = (m.lut_max + 1) * (LUT == 2 ? 4u : 1u);  // LUT words
+  const u32 lut_words = (lut_n + 1) & ~1u;                    // 8-B aligned s_tab
   // (direct tables hold (cum, c) themselves; then only the rare exact fix-up reads the table)
   constexpr bool tab_lds = !LUT || DEC_TAB_LDS;
   const uint2* s_tab = tab_lds ? reinterpret_cast<const uint2*>(s_dyn + lut_words) : m.tab;
   const u32 tid = threadIdx.x;
   if (tab_lds) reinterpret_cast<uint2*>(s_dyn + lut_words)[tid] = m.tab[tid];
-  for (u32 j = tid; j <= m.lut_max; j += WG) s_lut[j] = m.lut[j];
+  for (u32 j = tid; j < lut_n; j += WG) s_lut[j] = m.lut[j];
   __syncthreads();
   const u32 k = blockIdx.x * WG + tid;
   if (k >= n_chunks) return;
@@ -1142,6 +1149,18 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
     }
     while (lut.size() & (lut.size() - 1)) lut.push_back(lut.back());  // pow2 (masked index)
     a.lut_max = (u32)lut.size() - 1;
+    if (total_freq >= 256 && total_freq <= 512) {  // 16-B entries {cum, c, s, 0}
+      a.direct = 2;
+      std::vector<u32> wide(4 * lut.size());
+      for (size_t q = 0; q < lut.size(); ++q) {
+        const u32 sq = lut[q] & 255u;
+        wide[4 * q + 0] = cum_freq[sq];
+        wide[4 * q + 1] = c_freq[sq];
+        wide[4 * q + 2] = sq;
+        wide[4 * q + 3] = 0;
+      }
+      lut.swap(wide);
+    }
   }
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
@@ -1256,20 +1275,25 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
 #define RC_DEC_LAUNCH(D, S, L)                                                             \
   hipLaunchKernelGGL((k_decode_static<D, S, L>), grid, block, lut_bytes, ctx->cur, m->args, \
                      code, code_off, code_len, syms_out, sym_off, n_chunks, flags)
-  const bool dl = m->args.direct != 0;
+  const bool dl = m->args.direct != 0, dl2 = m->args.direct == 2;
   // dynamic LDS of k_decode_static: LUT (8-B aligned), the (cum, c) table, the code rings
-  const size_t lut_bytes = ((size_t)(m->args.lut_max + 2) & ~(size_t)1) * sizeof(u32) +
+  const size_t lut_n = ((size_t)m->args.lut_max + 1) * (dl2 ? 4 : 1);
+  const size_t lut_bytes = ((lut_n + 1) & ~(size_t)1) * sizeof(u32) +
                            (!dl || DEC_TAB_LDS ? 256 * sizeof(uint2) : 0) +
                            WAVES * DEC_RING_ALLOC * 64 * sizeof(u32);
 #ifdef RC_DEV_ONLY
   if (m->div != DIV_POW2 || !sm) return RC_E_ARG;
-  if (dl) RC_DEC_LAUNCH(DIV_POW2, 1, 1); else RC_DEC_LAUNCH(DIV_POW2, 1, 0);
+  if (dl2) RC_DEC_LAUNCH(DIV_POW2, 1, 2);
+  else if (dl) RC_DEC_LAUNCH(DIV_POW2, 1, 1); else RC_DEC_LAUNCH(DIV_POW2, 1, 0);
 #else
+  // (direct == 2 implies sm)
   if (m->div == DIV_POW2) {
-    if (sm) { if (dl) RC_DEC_LAUNCH(DIV_POW2, 1, 1); else RC_DEC_LAUNCH(DIV_POW2, 1, 0); }
+    if (dl2) RC_DEC_LAUNCH(DIV_POW2, 1, 2);
+    else if (sm) { if (dl) RC_DEC_LAUNCH(DIV_POW2, 1, 1); else RC_DEC_LAUNCH(DIV_POW2, 1, 0); }
     else    { if (dl) RC_DEC_LAUNCH(DIV_POW2, 0, 1); else RC_DEC_LAUNCH(DIV_POW2, 0, 0); }
   } else {
-    if (sm) { if (dl) RC_DEC_LAUNCH(DIV_MAGIC, 1, 1); else RC_DEC_LAUNCH(DIV_MAGIC, 1, 0); }
+    if (dl2) RC_DEC_LAUNCH(DIV_MAGIC, 1, 2);
+    else if (sm) { if (dl) RC_DEC_LAUNCH(DIV_MAGIC, 1, 1); else RC_DEC_LAUNCH(DIV_MAGIC, 1, 0); }
     else    { if (dl) RC_DEC_LAUNCH(DIV_MAGIC, 0, 1); else RC_DEC_LAUNCH(DIV_MAGIC, 0, 0); }
   }
 #endif

@@ -119,6 +119,46 @@ def test_random_models_vs_oracle(ctx, seed, kind):
         assert (dec[k] == ch).all(), k
 
 
+@pytest.mark.parametrize("total", [256, 300, 384, 511, 512])
+def test_wide_direct_lut_models(ctx, total):
+    """256 <= total <= 512 decodes through 16-B direct LUT entries {cum, c, s} (direct == 2):
+    pow2 and magic-division totals, zero frequencies, short alphabets; encode bytes, lengths
+    and decoded symbols against the oracle, and garbage streams decode like find_index."""
+    rng = np.random.default_rng(total)
+    n = int(rng.choice([3, 17, 200, 256]))
+    c = np.zeros(n, np.int64)
+    c[rng.choice(n, max(2, n - n // 6), replace=False)] = 1
+    while c.sum() < total:
+        c[int(rng.choice(np.nonzero(c)[0]))] += 1
+    c = c.astype(np.uint32)
+    cum = cum_of(c)
+    m = rc.StaticModel(c, cum, total)
+    nz = np.nonzero(c)[0]
+    p = c[nz] / c[nz].sum()
+    lens = list(rng.choice([0, 1, 15, 16, 63, 64, 65, 127, 128, 129, 1000, 4099], 64))
+    chunks = [rng.choice(nz, L, p=p).astype(np.uint8) for L in lens]
+    caps = [rc.slot_capacity(L, m.max_bits_per_symbol() + 1) for L in lens]
+    out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=True, seed=total)
+    codes = []
+    for k, ch in enumerate(chunks):
+        f, b, L = cpu.encode(c, cum, total, ch)
+        assert (fl[k], ol[k]) == (f, L), k
+        assert bytes(out[out_off[k]: out_off[k] + ol[k]]) == b, k
+        codes.append(b)
+    dec, fd = run_decode(m, codes, lens, misalign=True, seed=total + 1)
+    for k, ch in enumerate(chunks):
+        assert fd[k] == 0 and (dec[k] == ch).all(), k
+    garbage = [rng.integers(0, 256, int(rng.integers(8, 400))).astype(np.uint8).tobytes()
+               for _ in range(64)]
+    counts = [int(rng.integers(0, 300)) for _ in garbage]
+    dec, fd = run_decode(m, garbage, counts, misalign=False, seed=total + 2)
+    for k in range(len(garbage)):
+        f, d = cpu.decode(c, cum, total, garbage[k], counts[k])
+        assert fd[k] == f, k
+        if f == 0:
+            assert (dec[k] == d).all(), k
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_garbage_streams_decode_like_oracle(ctx, seed):
     """find_index on arbitrary bytes (data < lower_bound wraps, rfreq >= total) must pick the
