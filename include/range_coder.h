@@ -123,7 +123,9 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code_de
                           uint32_t* flags_dev);
 
 /* ---- synchronous host-memory helpers (stage through device memory, wait for completion;
- *      returns RC_E_CHUNK when any chunk is flagged — flags are still filled in) ---- */
+ *      returns RC_E_CHUNK when any chunk is flagged — flags are still filled in).  Their
+ *      staging buffers (4 x ~2 batches of ~1 GiB, on the context's device) stay allocated
+ *      with the context between calls and are freed by rc_ctx_destroy. ---- */
 rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
                          const uint64_t* sym_off, uint32_t n_chunks, uint8_t* out,
                          const uint64_t* out_off, uint64_t* out_len, uint32_t* flags);

@@ -1031,9 +1031,12 @@ rc_status rc_ctx_create(int device, rc_ctx** out) {
   return RC_OK;
 }
 
+void rc_stream_release_(const rc_ctx* ctx);  // rc_stream.hip: the cached host pipeline
+
 rc_status rc_ctx_destroy(rc_ctx* ctx) {
   if (!ctx) return RC_E_ARG;
   DeviceGuard g(ctx->device);
+  rc_stream_release_(ctx);
   (void)hipStreamSynchronize(ctx->own);
   (void)hipStreamSynchronize(ctx->cur);
   (void)hipFree(ctx->inv);

@@ -14,6 +14,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #define RC_STREAM_SLOTS 4
@@ -74,8 +76,17 @@ struct Pipe {
   u64* hlen = nullptr;              // pinned: n_chunks lengths (encode) / unused
   u32* hfl = nullptr;               // pinned: n_chunks flags
   bool ok = true;
+  int device = -1;
+  size_t c_in = 0, c_out = 0, c_off = 0;  // capacities this pipe was built for
+  u32 c_k = 0, c_n = 0;
 
+  bool fits(int dev, size_t in_max, size_t out_max, u32 kmax, u32 n_chunks, size_t n_off) const {
+    return ok && dev == device && in_max <= c_in && out_max <= c_out && kmax <= c_k &&
+           n_chunks <= c_n && n_off <= c_off;
+  }
   bool init(size_t in_max, size_t out_max, u32 kmax, u32 n_chunks, size_t n_off) {
+    (void)hipGetDevice(&device);
+    c_in = in_max, c_out = out_max, c_k = kmax, c_n = n_chunks, c_off = n_off;
     for (int i = 0; i < RC_STREAM_SLOTS; ++i) {
       ok = ok && hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) == hipSuccess;
       ok = ok && hipMalloc((void**)&din[i], in_max + 64) == hipSuccess;
@@ -106,6 +117,67 @@ struct Pipe {
     if (hoff) (void)hipHostFree(hoff);
     if (hlen) (void)hipHostFree(hlen);
     if (hfl) (void)hipHostFree(hfl);
+  }
+};
+
+// One pipeline per context, kept between calls: its ~8 GiB of device buffers and pinned arrays
+// cost far more to allocate than a batch takes to move (with most of HBM already allocated,
+// per-call hipMalloc / hipFree cut the encode path from 29 to 12 GB/s).  A call takes the
+// context's pipe out of the cache (so concurrent calls never share one), grows it if this
+// call needs more, and puts it back; rc_ctx_destroy frees it.
+std::mutex g_pipe_mu;
+std::unordered_map<const rc_ctx*, Pipe*> g_pipes;
+
+Pipe* pipe_acquire(const rc_ctx* ctx, int dev, size_t in_max, size_t out_max, u32 kmax,
+                   u32 n_chunks, size_t n_off) {
+  Pipe* p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    auto it = g_pipes.find(ctx);
+    if (it != g_pipes.end()) {
+      p = it->second;
+      g_pipes.erase(it);
+    }
+  }
+  if (p && p->fits(dev, in_max, out_max, kmax, n_chunks, n_off)) return p;
+  size_t a = in_max, b = out_max, e = n_off;
+  u32 c = kmax, d = n_chunks;
+  if (p && p->ok && p->device == dev) {  // grow to cover both the old and the new shape
+    a = std::max(a, p->c_in), b = std::max(b, p->c_out), e = std::max(e, p->c_off);
+    c = std::max(c, p->c_k), d = std::max(d, p->c_n);
+  }
+  delete p;
+  p = new Pipe;
+  if (!p->init(a, b, c, d, e)) {
+    delete p;
+    return nullptr;
+  }
+  return p;
+}
+
+void pipe_release(const rc_ctx* ctx, Pipe* p) {
+  if (!p) return;
+  if (!p->ok) {
+    delete p;
+    return;
+  }
+  Pipe* old = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    Pipe*& slot = g_pipes[ctx];
+    old = slot;
+    slot = p;
+  }
+  delete old;  // a concurrent call on the same context returned one first
+}
+
+// the pipe goes back to the cache on every return path
+struct PipeLease {
+  const rc_ctx* ctx;
+  Pipe* p;
+  ~PipeLease() {
+    if (p && !p->drain()) p->ok = false;
+    pipe_release(ctx, p);
   }
 };
 
@@ -179,10 +251,12 @@ rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
     kmax = std::max(kmax, b.k1 - b.k0);
     n_off += 3ull * (b.k1 - b.k0 + 1);
   }
-  Pipe p;
-  if (!p.init(in_max, out_max, kmax, n_chunks, n_off)) return RC_E_DEVICE;
+  // (the pins outlive the lease, whose destructor drains the streams on every return path)
   Pin pin_in(syms + sym_off[0], sym_off[n_chunks] - sym_off[0]);
   Pin pin_out(out + out_off[0], out_off[n_chunks] - out_off[0]);
+  PipeLease lease{ctx, pipe_acquire(ctx, dev, in_max, out_max, kmax, n_chunks, n_off)};
+  if (!lease.p) return RC_E_DEVICE;
+  Pipe& p = *lease.p;
   // the caller's stream must not run ahead into our buffers, nor we into its pending work
   (void)hipStreamSynchronize(s0);
   size_t o = 0;
@@ -246,10 +320,11 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
     cmin = std::min(cmin, b.in0);
     cmax = std::max(cmax, b.in1);
   }
-  Pipe p;
-  if (!p.init(in_max, out_max, kmax, n_chunks, n_off)) return RC_E_DEVICE;
   Pin pin_in(code + cmin, cmax - cmin);
   Pin pin_out(syms_out + sym_off[0], sym_off[n_chunks] - sym_off[0]);
+  PipeLease lease{ctx, pipe_acquire(ctx, dev, in_max, out_max, kmax, n_chunks, n_off)};
+  if (!lease.p) return RC_E_DEVICE;
+  Pipe& p = *lease.p;
   (void)hipStreamSynchronize(s0);
   size_t o = 0;
   for (size_t bi = 0; bi < bs.size(); ++bi) {
@@ -282,6 +357,20 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   if (!p.drain()) return RC_E_DEVICE;
   memcpy(flags, p.hfl, 4ull * n_chunks);
   return any_flag(flags, n_chunks);
+}
+
+// internal: free the context's cached pipeline (called by rc_ctx_destroy)
+void rc_stream_release_(const rc_ctx* ctx) {
+  Pipe* p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    auto it = g_pipes.find(ctx);
+    if (it != g_pipes.end()) {
+      p = it->second;
+      g_pipes.erase(it);
+    }
+  }
+  delete p;
 }
 
 }  // extern "C"
