@@ -104,3 +104,32 @@ def test_large_round_trip(ctx, pinned):
         assert bytes(hd[ooff[k]: ooff[k] + ol[k]]) == bytes(out[ooff[k]: ooff[k] + ol[k]])
     dec, fd = rc.decode_host(m, out, ooff[:-1], ol, soff)
     assert (fd == 0).all() and (dec == syms).all()
+
+
+def test_cached_pipeline_across_shapes(monkeypatch):
+    """The host pipeline is kept with its context: a small call, a larger one (the pipe grows),
+    a smaller one again (reused), then rc_ctx_destroy frees it; every call byte-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("RC_STREAM_BATCH_BYTES", "50000")
+    own = rc.Context(0)
+    try:
+        c, cum, total = synth.zipf_table()
+        m = rc.StaticModel(c, cum, total, ctx=own)
+        rng = np.random.default_rng(11)
+        p = np.asarray(c, float) / np.sum(c)
+        for n, hi in [(7, 500), (90, 4000), (3, 100)]:
+            lens, soff = layout(rng, n, 0, hi)
+            syms = rng.choice(256, int(soff[-1]), p=p).astype(np.uint8)
+            caps = np.array([rc.slot_capacity(int(L), m.max_bits_per_symbol()) for L in lens])
+            ooff = np.concatenate([[0], caps]).cumsum()
+            out, ol, fl = rc.encode_host(m, syms, soff, ooff)
+            assert (fl == 0).all()
+            for k in range(n):
+                f, b, L = cpu.encode(c, cum, total, syms[soff[k]: soff[k + 1]])
+                assert ol[k] == L and bytes(out[ooff[k]: ooff[k] + L]) == b, (n, k)
+            dec, fd = rc.decode_host(m, out, ooff[:-1], ol, soff)
+            assert (fd == 0).all() and (dec == syms).all(), n
+        del m
+    finally:
+        own.close()
