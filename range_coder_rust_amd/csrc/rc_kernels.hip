@@ -59,7 +59,7 @@ struct ModelArgs {
   u32 lut_max;       // number of buckets - 1
   float ftotal;      // (float)total
   u32 direct;        // 1: lut[q] = s | cum << 8 | c << 20 for every q < total (total <= 2048)
-                     // 2: lut[4q..4q+3] = {cum, c, s, 0} (256 <= total <= 512)
+                     // 2: lut[4q..4q+3] = {cum, c, s, total/c as f32} (256 <= total <= 512)
 };
 
 
@@ -479,6 +479,7 @@ struct Dec {
   // two 32-bit halves: as a u64 it must sit in an even-aligned VGPR pair, which costs a move
   // per symbol when its new halves are produced in other registers.
   u32 xlo, xhi;
+  float G;  // 16-B direct tables: 16 * total / (range / 2^32), carried from symbol to symbol
   __device__ __forceinline__ u64 x() const { return ((u64)xhi << 32) | xlo; }
   __device__ __forceinline__ void set_x(u64 v) { xlo = (u32)v; xhi = hi32(v); }
   u32 cpos;   // bytes consumed, relative to the 16-B aligned base of the code stream
@@ -637,6 +638,11 @@ static __device__ __forceinline__ u32 put_byte(u32 w, u32 v, int j) {
   return w;
 }
 
+// the hint scale of 16-B direct tables, exactly (from the top 32 bits of range)
+static __device__ __forceinline__ void dec_gexact(Dec& d, const ModelArgs& m) {
+  d.G = (16.0f * m.ftotal) * __builtin_amdgcn_rcpf(cvt_f32(hi32(d.range)));
+}
+
 template <int DIV, int SM, int LUT>
 static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const uint2* s_tab,
                                               const u32* s_lut) {
@@ -651,7 +657,10 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   // <= 2^-15 (and ~2^-24 for the usual range >= 2^56), far inside one frequency step.  Bucket
   // tables (totals up to 2^32) first shift both by clz(range), for a relative error ~2^-22.
   float X, R;
-  if (LUT) {
+  if (LUT == 2) {
+    X = cvt_f32(d.xhi);
+    R = 1.0f;  // unused: the scale G is carried
+  } else if (LUT) {
     X = cvt_f32(d.xhi);
     R = cvt_f32(hi32(d.range));
   } else {
@@ -663,14 +672,19 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   // entries, so an out-of-range hint (corrupt streams, x >= range; or rounding to q == total)
   // only starts the exact fix-up below from another symbol, whose result does not depend on
   // where it starts.  (A v_mul_f32 clamp modifier was tried instead and gave wrong hints.)
-  const float rR = __builtin_amdgcn_rcpf(R);
+  const float rR = LUT == 2 ? 1.0f : __builtin_amdgcn_rcpf(R);
   u32 s;
   uint2 t;
-  if (LUT == 2) {  // 16-B direct entries {cum, c, s}: one ds_read_b96 at byte 16q, no unpacking
-    const u32 q16 = cvt_u32_sat(X * ((16.0f * m.ftotal) * rR)) & (m.lut_max << 4);
-    const u32x3 ent = *(const __attribute__((address_space(3))) u32x3*)(uintptr_t)q16;
+  float tc = 0.0f;  // LUT == 2: total / c of the coded symbol, as a float
+  if (LUT == 2) {  // 16-B direct entries {cum, c, s, total/c}: one ds_read_b128, no unpacking
+    // G = 16 total / (range / 2^32) is not recomputed per symbol: range' = r c 2^k, so
+    // G' = G (total / c) 2^-k (one multiply, one ldexp instead of a convert and a reciprocal);
+    // it is recomputed exactly at every phase and after any rare path
+    const u32 q16 = cvt_u32_sat(X * d.G) & (m.lut_max << 4);
+    const u32x4 ent = *(const __attribute__((address_space(3))) u32x4*)(uintptr_t)q16;
     s = ent.z;
     t = make_uint2(ent.x, ent.y);
+    tc = __uint_as_float(ent.w);
   } else if (LUT) {  // direct table: candidate symbol and its (cum, c) in one LDS read at byte 4q
     // the LUT is the kernel's first LDS object (address 0): q4 is its LDS byte address
     const u32 q4 = cvt_u32_sat(X * ((4.0f * m.ftotal) * rR)) & (m.lut_max << 2);
@@ -693,6 +707,7 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   if (__builtin_expect(__any((int)(dx >= B)), 0)) {
     if (dx >= B) {
       dec_fix(s, t, A, B, d.x(), r, s_tab, m.n);
+      if (LUT == 2) tc = m.ftotal * __builtin_amdgcn_rcpf(cvt_f32(t.y));
       // the tables only hold symbols with c > 0, so c == 0 can only come from dec_fix: corrupt
       // input (the reference loops forever); an over-read, if any, came first
       if (t.y == 0) {
@@ -711,6 +726,7 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
                     : ((u32)__clzll(d.low ^ (d.low + d.range)) & 56u);
   d.low <<= k8;
   d.range <<= k8;
+  if (LUT == 2) d.G = __builtin_amdgcn_ldexpf(d.G * tc, -(int)k8);
   // data' = data << k8 | k settled bytes and low' = (low + A) << k8, so x' = ((x - A) << k8) |
   // those bytes (shift_left_buffer, decoder.rs:31-35): the high half of dx << k8, and the high
   // half of (dx_lo : next 4 code bytes) << k8 (alignbyte uses cpos & 3 only)
@@ -736,7 +752,10 @@ static __device__ __forceinline__ u32 dec_sym(Dec& d, const ModelArgs& m, const 
   const bool rare = SM ? (hi32(d.range) < 0x10000u)
                        : ((hi32(d.range) < 0x10000u) | ((int)(d.fill - d.cpos) < (int)DEC_NEED_WIDE));
   if (__builtin_expect(__any((int)rare), 0)) {
-    if (rare) dec_rare(d, SM ? DEC_NEED_SM : DEC_NEED_WIDE);
+    if (rare) {
+      dec_rare(d, SM ? DEC_NEED_SM : DEC_NEED_WIDE);
+      if (LUT == 2) dec_gexact(d, m);
+    }
   }
   return s;
 }
@@ -755,6 +774,7 @@ static __device__ __forceinline__ void dec_check4(Dec& d) {
 template <int DIV, int SM, int LUT>
 static __device__ __forceinline__ uint4 dec_phase16(Dec& d, const ModelArgs& m,
                                                     const uint2* s_tab, const u32* s_lut) {
+  if (LUT == 2) dec_gexact(d, m);  // bounds the drift of the carried scale to 16 symbols
   u32 w[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -822,6 +842,7 @@ __global__ __launch_bounds__(WG) void k_decode_static(
   }
   if (!d.pend_ok) dec_issue(d);
   d.set_x(dec_read8_before(d));  // data - low with low = 0
+  if (LUT == 2) dec_gexact(d, m);
 
   u64 i = 0;
   // head: single symbols until the output is 64-B aligned
@@ -1160,7 +1181,8 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
         wide[4 * q + 0] = cum_freq[sq];
         wide[4 * q + 1] = c_freq[sq];
         wide[4 * q + 2] = sq;
-        wide[4 * q + 3] = 0;
+        const float tcf = (float)total_freq / (float)c_freq[sq];
+        memcpy(&wide[4 * q + 3], &tcf, sizeof tcf);
       }
       lut.swap(wide);
     }
