@@ -1,0 +1,394 @@
+// rc_encode.hip — k_encode_static, the static-model encoder (see rc_static.h for the design
+// notes shared with the decoder).
+#include "rc_static.h"
+
+// ------------------------------------------------------------------------------------------
+// Encoder
+//
+// Per lane: one chunk.  Input: 64-symbol tiles (4 x 16 B per lane, issued one tile ahead).
+// Output: settled bytes are packed into dwords and pushed into a per-lane 128-B LDS ring every
+// symbol (unconditionally: when fewer than 4 bytes are ready the push writes the next, still
+// free, slot and does not advance).  HBM writes are cooperative: when any lane's ring holds
+// FLUSH_AT bytes, the wave runs a flush round in which every lane holding a complete 64-B unit
+// hands it over; each store instruction then writes 16 chunks x 64 B (whole 64-B units), which
+// the per-lane pattern (one 16-B granule of 64 different lines per instruction) cannot.
+// ------------------------------------------------------------------------------------------
+#define ENC_UNIT 64    // bytes per flush unit
+#define FLUSH_AT 88    // ring fill forcing a flush round: 88 + 7*3 + 3 + 11 (rare tail) < 124
+#define SINK_SLOTS 65536
+__device__ uint4 g_sink[SINK_SLOTS];  // dummy symbol tiles of dead lanes (contents irrelevant)
+
+struct Enc {
+  u64 low, range;  // RangeCoder state (range_coder.rs:7-12)
+  u64 acc;         // settled bytes, newest in the low bits; the B & 31 lowest are not pushed
+  u32 B;           // bit position of the next settled byte, from the 64-B aligned slot base:
+                   // dword B >> 5 of the stream is the incomplete one (its ring slot is free)
+  u32 fpos;        // byte position of the next unit to store
+  u32 err;         // first RC_F_* error of this chunk (SM: OR of staged table flags)
+  u32 ring;        // LDS byte address of this lane's ring column: dword j at ring + 256 * j.
+                   // The ring holds stream dwords as values (first byte in the top bits);
+                   // the flush rounds byte-swap them on the way out.
+};
+
+// ring dword `slot` of the lane whose column is at LDS byte address `col`
+static __device__ __forceinline__ void ring_put(u32 col, u32 slot, u32 v) {
+  *(__attribute__((address_space(3))) u32*)(uintptr_t)(col + (slot << 8)) = v;
+}
+
+// byte position of the incomplete dword (everything below it has been pushed to the ring)
+static __device__ __forceinline__ u32 enc_wpos(const Enc& e) { return (e.B >> 5) << 2; }
+
+// Per-chunk output geometry shared with the other lanes of the wave (flush rounds)
+struct EncOut {
+  uint8_t* gbase;  // 64-B aligned base of the slot
+  u32 lo_ok, hi_ok;  // writable byte window [lo_ok, hi_ok) relative to gbase
+};
+
+// One flush round.  Lane L of the wave moves granule (L & 3) of the unit of chunk 16*i + L/4
+// for i = 0..3; chunks with has == false are masked.  Granules touching the slot edges are
+// written byte by byte (first unit of a misaligned slot, capacity end).
+static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, const u32* wring,
+                                                 const EncOut* wout) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const u32 c = 16 * i + (lane >> 2), g = lane & 3;
+    const bool hc = __shfl((int)has, c) != 0;
+    const u32 fp = (u32)__shfl((int)e.fpos, c);
+    if (hc) {
+      const u32 slot = (fp >> 2) + 4 * g;
+      const u32* rp = wring + c;
+      const uint4 v = make_uint4(__builtin_bswap32(rp[((slot + 0) & (ENC_RING - 1)) * 64]),
+                                 __builtin_bswap32(rp[((slot + 1) & (ENC_RING - 1)) * 64]),
+                                 __builtin_bswap32(rp[((slot + 2) & (ENC_RING - 1)) * 64]),
+                                 __builtin_bswap32(rp[((slot + 3) & (ENC_RING - 1)) * 64]));
+      const EncOut o = wout[c];
+      const u32 p0 = fp + 16 * g;
+      if (p0 >= o.lo_ok && p0 + 16 <= o.hi_ok) {
+        u32x4 g16;
+        g16.x = v.x;
+        g16.y = v.y;
+        g16.z = v.z;
+        g16.w = v.w;
+        gstore128(o.gbase + p0, g16);
+      } else {
+        const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const u32 p = p0 + j;
+          if (p >= o.lo_ok && p < o.hi_ok) gstore8(o.gbase + p, w[j >> 2] >> (8 * (j & 3)));
+        }
+      }
+    }
+  }
+  e.fpos += has ? (u32)ENC_UNIT : 0u;
+}
+
+// flush rounds until no lane's ring is above the threshold (wave-uniform call sites only)
+static __device__ __forceinline__ void enc_flush(Enc& e, u32 lane, const u32* wring,
+                                                 const EncOut* wout) {
+  while (__any((int)(enc_wpos(e) - e.fpos >= FLUSH_AT)))
+    enc_round(e, enc_wpos(e) - e.fpos >= ENC_UNIT, lane, wring, wout);
+}
+
+// One settled byte, with a conditional push (rare paths only).
+static __device__ __forceinline__ void enc_emit_byte(Enc& e, u32 b) {
+  e.acc = (e.acc << 8) | b;
+  e.B += 8;
+  if ((e.B & 31) == 0) ring_put(e.ring, ((e.B >> 5) - 1) & (ENC_RING - 1), (u32)e.acc);
+}
+
+// Rare tail of param_update for one lane: the no-carry loop when >= 4 bytes settle
+// (range_coder.rs:110-116, continued byte by byte) and range_reduction_expansion (:126-135).
+static __device__ __forceinline__ void enc_rare(Enc& e) {
+  while (((e.low ^ (e.low + e.range)) >> 56) == 0) {
+    enc_emit_byte(e, (u32)(e.low >> 56));
+    e.low <<= 8;
+    e.range <<= 8;
+  }
+  while (e.range < TOP16) {
+    e.range = ~e.low & (TOP16 - 1);
+    enc_emit_byte(e, (u32)(e.low >> 56));
+    e.low <<= 8;
+    e.range <<= 8;
+  }
+}
+
+// Encoder::encode (encoder.rs:24-37) -> RangeCoder::param_update (range_coder.rs:53-92),
+// common path without branches.  Returns true when the lane needs enc_rare().  Written for the
+// gfx950 VALU price list (profiles/r01/ubench_valu.txt): 64-bit ops, multiplies, compares and
+// bit-field ops cost ~3.6 cycles per wave, plain 32-bit add/logic/right-shift ~2.
+// SM: 0 wide model; 1 small model (256 <= total <= 2^16) that may hold entries the reference
+// cannot encode; 2 small and complete (256 symbols, every c > 0: nothing to check)
+template <int DIV, int SM>
+static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint2 t) {
+  u32 c, cum;
+  if (SM == 2) {
+    cum = t.x;
+    c = t.y;
+  } else if (SM) {  // bad entries were staged as (flag << 24, 1): accumulate, sort out at the end
+    // (as an asm OR: left to itself the compiler defers all the ORs to the end of the loop
+    // and spills every table entry)
+    asm volatile("v_or_b32 %0, %0, %1" : "+v"(e.err) : "v"(t.x));
+    cum = t.x & 0xFFFFFFu;
+    c = t.y;
+  } else {
+    const bool bad = t.y == 0;  // zero frequency (reference: endless loop) or outside alphabet
+    const u32 code = t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ;
+    e.err = (bad && e.err == 0) ? code : e.err;
+    c = bad ? 1u : t.y;
+    cum = bad ? 0u : t.x;
+  }
+  const u64 r = range_par_total<DIV>(e.range, m);
+  if (SM) {  // r < 2^56, c, cum <= 2^16: low half by v_mad_u64_u32, high by v_mad_u32_u24
+    const u32 rl = (u32)r, rh = hi32(r);
+    const u64 R0 = (u64)rl * c;                   // range_coder.rs:65
+    const u64 L0 = (u64)rl * cum + e.low;         // range_coder.rs:68-81 (no overflow, §3)
+    e.range = ((u64)(hi32(R0) + __umul24(rh, c)) << 32) | (u32)R0;
+    e.low = ((u64)(hi32(L0) + __umul24(rh, cum)) << 32) | (u32)L0;
+  } else {
+    e.range = r * (u64)c;
+    e.low += r * (u64)cum;
+  }
+  // no_carry_expansion in closed form: k = clz(low ^ upper) / 8 bytes settle (<= 3 here;
+  // equal high halves (ffbh = ~0) mean >= 4 and the rare path continues after these 3)
+  const u32 lh = hi32(e.low);
+  const u32 z = ffbh(lh ^ hi32(e.low + e.range));
+  const u32 nb = z & 24u;
+  const u32 bytes = __builtin_amdgcn_ubfe(lh, 32u - nb, nb);  // the top nb bits (0 if nb == 0)
+  e.acc = (e.acc << nb) | bytes;
+  e.low <<= nb;
+  e.range <<= nb;
+  // push: the slot of the dword that was incomplete before this symbol gets the 32 bits above
+  // the (new) incomplete ones; if it is still incomplete the slot is rewritten later
+  const u32 slot = __builtin_amdgcn_ubfe(e.B, 5, 5);  // (B >> 5) & (ENC_RING - 1): v_bfe_u32
+  e.B += nb;
+  ring_put(e.ring, slot, (u32)(e.acc >> (e.B & 31u)));
+  // SM: range >= 2^32 after narrowing, so the high halves differ (z <= 31) and at most 3 bytes
+  // settle; only range_reduction_expansion can be pending
+  if (SM) return hi32(e.range) < 0x10000u;
+  return (z > 31u) | (hi32(e.range) < 0x10000u);
+}
+
+// one symbol (table entry t) for the lanes with `act`; the rare path (wave-uniform branch) may
+// flush
+template <int DIV, int SM>
+static __device__ __forceinline__ void enc_sym(Enc& e, const ModelArgs& m, uint2 t, bool act,
+                                               u32 lane, const u32* wring, const EncOut* wout) {
+  bool rare = false;
+  if (act) rare = enc_step<DIV, SM>(e, m, t);
+  if (__builtin_expect(__any((int)rare), 0)) {
+    if (rare) enc_rare(e);
+    enc_flush(e, lane, wring, wout);
+  }
+}
+
+// 16 symbols from one 16-B load, a flush check after every 8 (wave-uniform).  The table entry
+// of the next symbol is read before the current symbol is coded, so the LDS latency is off the
+// range -> range dependency chain.
+template <int DIV, int SM>
+static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const uint2* s_tab,
+                                             uint4 v, bool act, u32 lane, const u32* wring,
+                                             const EncOut* wout) {
+  // the words rotate down (w0 holds the current 4 symbols) instead of being indexed: a rolled
+  // loop would select w[i >> 2] with v_cndmask_b32 on VCC (~13 extra SIMD cycles each)
+  u32 w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+  uint2 t = s_tab[w0 & 255u];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u32 sn = i < 3 ? (w0 >> (8 * (i + 1))) & 255u : w1 & 255u;
+      const uint2 tn = s_tab[sn];  // (past the tile's end: a harmless extra read)
+      enc_sym<DIV, SM>(e, m, t, act, lane, wring, wout);
+      t = tn;
+    }
+    if (q & 1) enc_flush(e, lane, wring, wout);
+    w0 = w1;
+    w1 = w2;
+    w2 = w3;
+  }
+}
+
+// one symbol fetched byte-wise (unaligned head / tail of a chunk)
+template <int DIV, int SM>
+static __device__ __forceinline__ void enc_byte_sym(Enc& e, const ModelArgs& m,
+                                                    const uint2* s_tab, const uint8_t* sp, u64 i,
+                                                    bool act, u32 lane, const u32* wring,
+                                                    const EncOut* wout) {
+  const u32 sym = act ? (u32)sp[i] : 0u;
+  enc_sym<DIV, SM>(e, m, s_tab[sym], act, lane, wring, wout);
+}
+
+// the first symbol of a chunk the reference cannot encode (rare: flagged chunks only)
+static __device__ u32 enc_first_error(const ModelArgs& m, const uint8_t* sp, u64 n) {
+  for (u64 i = 0; i < n; ++i) {
+    const u32 s = sp[i];
+    if (s >= m.n) return RC_F_BAD_SYMBOL;  // sample_impl.rs:19 (Vec::get().unwrap())
+    if (m.tab[s].y == 0) return RC_F_ZERO_FREQ;  // range_coder.rs:83-85 (endless loop)
+  }
+  return 0;
+}
+
+template <int DIV, int SM>
+__global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint8_t* __restrict__ syms,
+                                                        const u64* __restrict__ sym_off,
+                                                        u32 n_chunks, uint8_t* __restrict__ out,
+                                                        const u64* __restrict__ out_off,
+                                                        u64* __restrict__ out_len,
+                                                        u32* __restrict__ flags) {
+  __shared__ uint2 s_tab[256];
+  __shared__ u32 s_ring[WAVES * ENC_RING * 64];
+  __shared__ EncOut s_out[WG];
+  const u32 tid = threadIdx.x;
+  {
+    // SM (cum < 2^16): a symbol the reference cannot encode (c == 0: endless loop; outside the
+    // alphabet: panic) is staged as (flag << 24, c = 1), so the common path only ORs entries
+    // together; a chunk whose OR shows a flag is re-scanned for its first error at the end
+    uint2 t = m.tab[tid];
+    if (SM == 1 && t.y == 0)
+      t = make_uint2((t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ) << 24, 1u);
+    s_tab[tid] = t;
+  }
+  const u32 lane = tid & 63, wave = tid >> 6;
+  const u32 k = blockIdx.x * WG + tid;
+  const bool live = k < n_chunks;  // dead lanes still take part in the wave's flush rounds
+  RC_VGPR_FLOOR_128();
+
+  u64 s0 = 0, n = 0, o0 = 0, o1 = 0;
+  if (live) {
+    s0 = sym_off[k];
+    n = sym_off[k + 1] - s0;
+    o0 = out_off[k];
+    o1 = out_off[k + 1];
+  }
+  const u32 a = (u32)(((uintptr_t)out + o0) & (ENC_UNIT - 1));
+  u64 cap = o1 - o0;
+  if (cap > 0xFFFFFF00ull - a) cap = 0xFFFFFF00ull - a;
+  s_out[tid].gbase = out + o0 - a;
+  s_out[tid].lo_ok = a;
+  s_out[tid].hi_ok = a + (u32)cap;
+  __syncthreads();
+  const u32* wring = s_ring + wave * ENC_RING * 64;
+  const EncOut* wout = s_out + wave * 64;
+
+  Enc e;
+  e.low = 0;  // RangeCoder::default (range_coder.rs:13-20)
+  e.range = ~0ull;
+  e.acc = 0;
+  e.B = 8 * a;  // pad bytes in front of the slot (never stored)
+  e.fpos = 0;
+  e.err = 0;
+  e.ring = (u32)(uintptr_t)(__attribute__((address_space(3))) u32*)(s_ring + wave * ENC_RING * 64 + lane);
+
+  const uint8_t* sp = syms + s0;
+  u64 head = (64 - ((uintptr_t)sp & 63)) & 63;  // symbols before the first 64-B aligned tile
+  if (head > n) head = n;
+  const u64 ntile = (n - head) >> 6;
+  // head: byte-wise, all lanes in step (flush rounds are wave-wide)
+  for (u64 i = 0; __any((int)(i < head)); ++i) {
+    enc_byte_sym<DIV, SM>(e, m, s_tab, sp, i, i < head, lane, wring, wout);
+    if ((i & 7) == 7) enc_flush(e, lane, wring, wout);
+  }
+  // body, part 1: the tiles every live lane of the wave has, with every lane active (no
+  // per-symbol exec masking).  Dead lanes run along on a dummy tile (g_sink, zeros) and a slot
+  // with no writable bytes; their results are dropped.
+  u64 tm = live ? ntile : ~0ull;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const u64 v = ((u64)(u32)__shfl_xor((int)hi32(tm), o) << 32) | (u32)__shfl_xor((int)(u32)tm, o);
+    tm = v < tm ? v : tm;
+  }
+  if (tm == ~0ull) tm = 0;  // no live lane in this wave
+  const u64 tmin = ((u64)__builtin_amdgcn_readfirstlane(hi32(tm)) << 32) |
+                   __builtin_amdgcn_readfirstlane((u32)tm);  // wave-uniform (scalar) trip count
+  const uint4* tp = live ? reinterpret_cast<const uint4*>(sp + head)
+                         : reinterpret_cast<const uint4*>(g_sink);
+  const u64 tstep = live ? 4 : 0;  // uint4s per tile
+  uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0;
+  if (tmin) {
+    c0 = tp[0];
+    c1 = tp[1];
+    c2 = tp[2];
+    c3 = tp[3];
+  }
+  for (u64 t = 0; t < tmin; ++t) {
+    uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
+    if (t + 1 < tmin) {
+      const uint4* q = tp + (t + 1) * tstep;
+      n0 = q[0];
+      n1 = q[1];
+      n2 = q[2];
+      n3 = q[3];
+    }
+    enc16<DIV, SM>(e, m, s_tab, c0, true, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c1, true, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c2, true, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c3, true, lane, wring, wout);
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
+  }
+  // body, part 2 (ragged waves): the remaining 16-symbol blocks of the tiles, lanes masked
+  const u64 nblk = ntile * 4;
+  for (u64 b = tmin * 4; __any((int)(b < nblk)); ++b) {
+    const bool act = b < nblk;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (act) v = tp[b];
+    enc16<DIV, SM>(e, m, s_tab, v, act, lane, wring, wout);
+  }
+  const u64 tail0 = head + (ntile << 6);
+  for (u64 j = 0; __any((int)(tail0 + j < n)); ++j) {  // j is wave-uniform
+    enc_byte_sym<DIV, SM>(e, m, s_tab, sp, tail0 + j, tail0 + j < n, lane, wring, wout);
+    if ((j & 7) == 7) enc_flush(e, lane, wring, wout);
+  }
+
+  // Encoder::finish (encoder.rs:40-46): 8 x left_shift
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    enc_emit_byte(e, (u32)(e.low >> 56));
+    e.low <<= 8;
+  }
+  const u32 len = (e.B >> 3) - a;
+  u32 wend = enc_wpos(e);
+  if (e.B & 31) {  // the last, incomplete dword
+    ring_put(e.ring, (e.B >> 5) & (ENC_RING - 1), (u32)(e.acc << (32 - (e.B & 31))));
+    wend += 4;
+  }
+  // final rounds: the last (partial) units, clipped to the stream end
+  const u32 end = a + len;
+  if (end < s_out[tid].hi_ok) s_out[tid].hi_ok = end;
+  while (__any((int)(e.fpos < wend))) enc_round(e, e.fpos < wend, lane, wring, wout);
+  if (live) {
+    if (SM == 1) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
+    if (!e.err && (u64)len > cap) e.err = RC_F_CAPACITY;
+    out_len[k] = len;
+    flags[k] = e.err;
+  }
+}
+
+
+hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a, int div, int smv,
+                                   const uint8_t* syms, const u64* sym_off, u32 n_chunks,
+                                   uint8_t* out, const u64* out_off, u64* out_len, u32* flags) {
+  const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
+#define RC_ENC_LAUNCH(D, S)                                                                   \
+  hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, stream, a, syms, sym_off,      \
+                     n_chunks, out, out_off, out_len, flags)
+#ifdef RC_DEV_ONLY  // scratch builds for kernel tuning: the headline variants only
+  if (div != DIV_POW2 || smv == 0) return hipErrorInvalidValue;
+  if (smv == 2) RC_ENC_LAUNCH(DIV_POW2, 2); else RC_ENC_LAUNCH(DIV_POW2, 1);
+#else
+  if (div == DIV_POW2) {
+    if (smv == 2) RC_ENC_LAUNCH(DIV_POW2, 2);
+    else if (smv == 1) RC_ENC_LAUNCH(DIV_POW2, 1);
+    else RC_ENC_LAUNCH(DIV_POW2, 0);
+  } else {
+    if (smv == 2) RC_ENC_LAUNCH(DIV_MAGIC, 2);
+    else if (smv == 1) RC_ENC_LAUNCH(DIV_MAGIC, 1);
+    else RC_ENC_LAUNCH(DIV_MAGIC, 0);
+  }
+#endif
+#undef RC_ENC_LAUNCH
+  return hipGetLastError();
+}

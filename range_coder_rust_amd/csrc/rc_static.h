@@ -1,0 +1,115 @@
+// rc_static.h — shared definitions of the static-model kernels (rc_encode.hip, rc_decode.inc).
+//
+// One independent stream ("chunk", a fresh reference Encoder/Decoder) per lane; 64 chunks per
+// wave run the reference's sequential per-symbol loop in lock-step.  The arithmetic restates
+// src/range_coder.rs (param_update :53-92, left_shift :95-100, no_carry_expansion :110-116,
+// range_reduction_expansion :126-135), src/encoder.rs (encode :24-37, finish :40-46) and
+// src/decoder.rs (new :14-23, decode :38-54) bit-exactly, with these MI355X-specific choices:
+//  * coder state (lower_bound, range, decoder data window) lives in VGPR pairs;
+//  * the PModel snapshot (cum, c) and the decoder's inverse-CDF table live in LDS;
+//  * the no-carry loop (range_coder.rs:83-85) is evaluated in closed form: it settles exactly
+//    k = clz64(low ^ (low + range)) / 8 bytes (proof in DESIGN.md §3), so the wave does not
+//    diverge on it;
+//  * range / total (range_coder.rs:38-40) is a shift for power-of-two totals and an exact
+//    multiply-high by a host-computed reciprocal otherwise (no 64-bit divide on the VALU);
+//  * the decoder's find_index division + binary search (sample_impl.rs:27-45) is replaced by a
+//    float hint -> LDS inverse-CDF table -> exact integer verification r*cum[s] <= data-low <
+//    r*cum[s+1], which yields the same index for every input, valid or corrupt;
+//  * encoder: symbols are read 64 B per lane per tile; settled bytes go through a per-lane LDS
+//    ring and are written by cooperative flush rounds, 16 chunks x 64 B per store instruction;
+//  * decoder: the code is read 64 B per lane into a per-lane LDS ring one 16-symbol phase
+//    ahead; decoded symbols are written 16 B per lane per phase.
+#pragma once
+#include "rc_common.h"
+
+#define WG 256
+#define WAVES (WG / 64)
+#define ENC_RING 32          // dwords per lane in the encoder's output ring (128 B)
+#ifndef DEC_RING
+#define DEC_RING 16          // dwords per lane in the decoder's input ring (64 B)
+#endif
+#ifndef DEC_MIRROR
+#define DEC_MIRROR 2         // mirror slots past the ring, so a 3-dword read never wraps
+#endif
+#define DEC_RING_ALLOC (DEC_RING + DEC_MIRROR)
+#ifndef DEC_PF
+#define DEC_PF 2             // 16-B blocks per ring refill (32 B, one 16-symbol phase ahead)
+#endif
+#ifndef DEC_LD
+#define DEC_LD 4             // 16-B blocks per global load burst (64 B: two refills)
+#endif
+#ifndef DEC_OUT_BURST
+#define DEC_OUT_BURST 4      // 16-B symbol blocks per lane per output burst (4: 64 B)
+#endif
+#ifndef DEC_TAB_LDS
+#define DEC_TAB_LDS 1        // direct-LUT decoders: keep the (cum, c) table in LDS too
+#endif
+#define LUT_BITS 12
+#define LUT_MAX_ENTRIES (1u << LUT_BITS)
+
+enum { DIV_POW2 = 0, DIV_MAGIC = 1 };
+
+struct ModelArgs {
+  const uint2* tab;  // [256] (cum, c); entries s >= n_symbols hold (0xFFFFFFFF, 0)
+  const u32* lut;    // decoder buckets: s0 | s1 << 8 | split << 16
+  u64 magic;         // floor((2^64 - 1) / total) for DIV_MAGIC
+  u32 n;             // alphabet size (1..256)
+  u32 total;         // total_freq
+  u32 lg;            // log2(total) for DIV_POW2
+  u32 lut_shift;     // bucket = q >> lut_shift
+  u32 lut_max;       // number of buckets - 1
+  float ftotal;      // (float)total
+  u32 direct;        // 1: lut[q] = s | cum << 8 | c << 20 for every q < total (total <= 2048)
+                     // 2: lut[4q..4q+3] = {cum, c, s, total/c as f32} (256 <= total <= 512)
+};
+
+
+// RangeCoder::range_par_total (range_coder.rs:38-40): range / total, exact.
+template <int DIV>
+static __device__ __forceinline__ u64 range_par_total(u64 range, const ModelArgs& m) {
+  if (DIV == DIV_POW2) return range >> m.lg;
+  u64 q = __umul64hi(range, m.magic);  // q in {floor - 1, floor}
+  u64 rem = range - q * (u64)m.total;
+  return rem >= (u64)m.total ? q + 1 : q;
+}
+
+// r * v for the coder's products (range_coder.rs:65, :70).  SM (256 <= total <= 2^16): r < 2^56
+// and v <= 2^16, so the high half is a 24-bit multiply.  SM is written out as two
+// instructions, lo(r)*v as a 64-bit product plus a 24-bit mad into its high half: from the C
+// form the compiler re-derives the low half with an extra v_mul_lo_u32 and zeroes the mad's
+// addend with two moves (three extra VALU per product).
+template <int SM>
+static __device__ __forceinline__ u64 mul_rv(u64 r, u32 v) {
+  if (SM) {
+    u64 p, c;
+    u32 h;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(c) : "v"((u32)r), "v"(v));
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(r)), "v"(v), "v"(hi32(p)));
+    return ((u64)h << 32) | (u32)p;
+  }
+  return r * (u64)v;
+}
+
+
+// v_ffbh_u32 as the hardware defines it: 0xFFFFFFFF for 0 (the clz builtins are undefined there)
+static __device__ __forceinline__ u32 ffbh(u32 v) {
+  u32 r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// launchers (one translation unit each, so the variants compile in parallel)
+hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a, int div, int smv,
+                                   const uint8_t* syms, const u64* sym_off, u32 n_chunks,
+                                   uint8_t* out, const u64* out_off, u64* out_len, u32* flags);
+// dynamic LDS bytes of k_decode_static for a model
+size_t rc_static_decode_lds(const ModelArgs& a);
+hipError_t rc_static_decode_launch_pow2(hipStream_t stream, const ModelArgs& a, int sm,
+                                        const uint8_t* code, const u64* code_off,
+                                        const u64* code_len, uint8_t* syms_out,
+                                        const u64* sym_off, u32 n_chunks, u32* flags);
+hipError_t rc_static_decode_launch_magic(hipStream_t stream, const ModelArgs& a, int sm,
+                                         const uint8_t* code, const u64* code_off,
+                                         const u64* code_len, uint8_t* syms_out,
+                                         const u64* sym_off, u32 n_chunks, u32* flags);
+
