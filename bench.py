@@ -7,12 +7,14 @@ PModel (c[i] = 1, total 256), synthetic symbols generated in HBM.  One step = en
 (Decoder::new + 65,536 x decode, decoder.rs:14-54), all inputs resident in HBM.
 value = symbols round-tripped / second over all ranks = N_sym / (t_enc + t_dec), Gsymbols/s.
 
-N > 1 (torchrun, one process per GPU): every rank codes its own 2^20 chunks (chunks are
-independent streams — no data-path collective; weak scaling): rank r holds global chunks
-[r * 2^20, (r + 1) * 2^20) of one synthetic stream.  With --global-chunks G the G chunks are
-sharded instead (configs[4]: a fixed stream split over the GPUs; strong scaling).  The
-torch.distributed process group (RCCL) is used only for the barrier and the max-over-ranks of
-the timed region (range_coder_rust_amd/shard.py).
+N > 1 (one process per GPU): `bench.py --gpus N` launches its N ranks itself (torch.distributed.run
+on 127.0.0.1, before any GPU call), or runs as one rank of an external torchrun whose WORLD_SIZE
+must equal N.  The N > 1 line is configs[4]: one fixed 64 GiB Zipf(1.2) stream of 2^20 x 64 KiB
+chunks split into contiguous shards over the ranks (strong scaling; chunks are independent
+streams, encoder.rs:48-55, so there is no data-path collective).  The uniform configs[1] load of
+2^20 chunks per rank (weak scaling) is reported beside it under extras.uniform_weak.  The
+torch.distributed process group (RCCL) carries only the barriers, the max-over-ranks of the timed
+region and the all-ranks-bit-exact flag (range_coder_rust_amd/shard.py).
 
 Also reported: the Zipf(1.2) configuration (configs[2]) on the same buffers, per-kernel times,
 the HBM roofline of the dominant kernel and a CPU baseline (the C oracle on the host cores,
@@ -30,19 +32,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CTRL_DEVICE = "cuda"  # where the barrier / max-over-ranks tensors live (RCCL)
 SEED = 0x5EED0001
 
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (ranks) of this node; default WORLD_SIZE or 1")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU")
-    p.add_argument("--global-chunks", type=int, default=0,
-                   help="shard this many chunks over the ranks instead (strong scaling)")
+    p.add_argument("--global-chunks", type=int, default=None,
+                   help="shard this many chunks over the ranks instead (strong scaling); "
+                        "default 2^20 (configs[4]) when N > 1, else off")
     p.add_argument("--chunk-bytes", type=int, default=65536)
-    p.add_argument("--config", choices=["uniform", "zipf"], default="uniform")
+    p.add_argument("--config", choices=["uniform", "zipf"], default=None,
+                   help="default: uniform (configs[1]) at N = 1, zipf (configs[4]) at N > 1")
     p.add_argument("--no-zipf", action="store_true", help="skip the secondary Zipf leg")
     p.add_argument("--no-adaptive", action="store_true", help="skip the adaptive (C4) leg")
     p.add_argument("--no-model-build", action="store_true",
@@ -53,7 +59,8 @@ def parse():
                    help="skip the host-resident (PCIe) encode/decode leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU sample wall time")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="0 = every CPU this process may run on (affinity and cgroup quota)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return p.parse_args()
@@ -81,11 +88,12 @@ class Leg:
         dev = torch.device("cuda", ctx.device)
         self.cap = cap
         if bufs is None:
-            bufs = dict(syms=torch.empty(n * L, dtype=torch.uint8, device=dev),
-                        out=torch.empty(n * cap, dtype=torch.uint8, device=dev),
-                        dec=torch.empty(n * L, dtype=torch.uint8, device=dev))
+            bufs = Leg.alloc(torch, dev, n, L)
+        if n * L > bufs["syms"].numel() or n * cap > bufs["out"].numel():
+            raise ValueError("leg does not fit the shared arena")
         self.bufs = bufs
-        self.syms, self.out, self.dec = bufs["syms"], bufs["out"], bufs["dec"]
+        self.syms, self.out = bufs["syms"][: n * L], bufs["out"][: n * cap]
+        self.dec = bufs["dec"][: n * L]
         self.inv = synth.inverse_cdf(c)
         from range_coder_rust_amd import shard
         self.seed = shard.synth_seed(SEED, first_chunk)  # this rank's slice of one global stream
@@ -97,6 +105,16 @@ class Leg:
         self.fenc = torch.zeros(n, dtype=torch.int32, device=dev)
         self.fdec = torch.zeros(n, dtype=torch.int32, device=dev)
         self.rc = rc
+
+    @staticmethod
+    def alloc(torch, dev, n, L):
+        """Symbols, code slots (at the uniform model's 8 bits/symbol) and decoded symbols for
+        n chunks of L symbols; every leg takes prefixes of these."""
+        from range_coder_rust_amd import api
+        cap = api.slot_capacity(L, 8.0, slack=1.02)
+        return dict(syms=torch.empty(n * L, dtype=torch.uint8, device=dev),
+                    out=torch.empty(n * cap, dtype=torch.uint8, device=dev),
+                    dec=torch.empty(n * L, dtype=torch.uint8, device=dev))
 
     def encode(self):
         self.rc.encode_batch(self.model, self.syms, self.sym_off, self.out, self.out_off,
@@ -143,10 +161,11 @@ def run_leg(torch, dist, leg, steps, warmup, world):
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     from range_coder_rust_amd import shard
-    t = shard.max_over_ranks(t, dist if world > 1 else None, device="cuda")
+    t = shard.max_over_ranks(t, dist if world > 1 else None, device=CTRL_DEVICE)
     # correctness of the timed work: no chunk flagged, decode(encode(x)) == x
     ok = (int(leg.fenc.abs().sum()) == 0 and int(leg.fdec.abs().sum()) == 0
           and equal_chunked(torch, leg.dec, leg.syms))
+    ok = shard.all_ranks_true(ok, dist if world > 1 else None, device=CTRL_DEVICE)
     code_bytes = int(leg.out_len.sum())
     return dict(t=t, enc_ms=enc_ms, dec_ms=dec_ms, ok=ok, code_bytes=code_bytes)
 
@@ -267,57 +286,120 @@ def host_stream_leg(torch, rc, leg, n_chunks):
     return res
 
 
+def host_cpus():
+    """(nproc, usable): os.cpu_count(), and the CPUs this process may actually run on — its
+    affinity mask, capped by a cgroup v2 CPU quota (a GPU box's share of a larger host)."""
+    nproc = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = nproc
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            usable = min(usable, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return nproc, usable
+
+
 def cpu_baseline(torch, leg, seconds, threads):
-    """The C oracle (a bit-exact restatement of the Rust reference) on host cores, on a bounded
-    sample of the same chunks (copied from HBM), encode + decode, Gsymbols/s round trip."""
+    """The C oracle (a bit-exact restatement of the Rust reference; no rustc here) on the host,
+    on bounded samples of the same chunks (copied from HBM), encode + decode, Gsymbols/s round
+    trip: on every usable CPU (one chunk per task, as independent Encoders would run), and on
+    one core."""
     from oracle import cpu
     L = leg.L
 
-    def run(S):
+    def run(S, th, check):
         syms = leg.syms[: S * L].cpu().numpy()
         so = (np.arange(S + 1) * L).astype(np.uint64)
         oo = (np.arange(S + 1) * leg.cap).astype(np.uint64)
         t0 = time.perf_counter()
-        out, ol, fl = cpu.encode_batch(leg.c, leg.cum, leg.total, syms, so, oo, threads)
+        out, ol, fl = cpu.encode_batch(leg.c, leg.cum, leg.total, syms, so, oo, th)
         t1 = time.perf_counter()
-        dec, fd = cpu.decode_batch(leg.c, leg.cum, leg.total, out, oo[:-1], ol, so, threads)
+        dec, fd = cpu.decode_batch(leg.c, leg.cum, leg.total, out, oo[:-1], ol, so, th)
         t2 = time.perf_counter()
         assert (fl == 0).all() and (fd == 0).all() and (dec == syms).all()
-        # the CPU stream equals the GPU stream byte for byte on the sample's first chunks
-        g = leg.out[: leg.cap * min(S, 8)].cpu().numpy()
-        for k in range(min(S, 8)):
-            assert bytes(g[k * leg.cap: k * leg.cap + int(ol[k])]) == \
-                bytes(out[k * leg.cap: k * leg.cap + int(ol[k])])
+        if check:  # the CPU stream equals the GPU stream byte for byte on the first chunks
+            g = leg.out[: leg.cap * min(S, 8)].cpu().numpy()
+            for k in range(min(S, 8)):
+                assert bytes(g[k * leg.cap: k * leg.cap + int(ol[k])]) == \
+                    bytes(out[k * leg.cap: k * leg.cap + int(ol[k])])
         return t1 - t0, t2 - t1
 
+    nproc, usable = host_cpus()
+    threads = threads or usable
     S0 = max(threads, 16)
-    te, td = run(S0)
-    S = int(min(leg.n, max(S0, min(32768, S0 * seconds / max(te + td, 1e-6)))))
+    te, td = run(S0, threads, True)
+    S = int(min(leg.n, max(S0, min(65536, S0 * seconds / max(te + td, 1e-6)))))
     S = max(threads, S // threads * threads)
-    te, td = run(S)
+    te, td = run(S, threads, False)
     n_sym = S * L
+    # one core: a smaller sample (~1/4 of the time budget)
+    te1, td1 = run(2, 1, False)
+    S1 = int(max(2, min(256, 2 * seconds / 4 / max(te1 + td1, 1e-6))))
+    te1, td1 = run(S1, 1, False)
     return dict(value=n_sym / (te + td) / 1e9, unit="Gsymbols/s", cores=threads, kind="port",
+                nproc=nproc, usable_cpus=usable,
                 sample=f"{S} of the {leg.n} 64 KiB chunks ({n_sym} symbols), encode+decode by "
-                       f"the C oracle on {threads} host threads: enc {n_sym / te / 1e9:.4f} "
-                       f"Gsym/s, dec {n_sym / td / 1e9:.4f} Gsym/s",
-                encode=n_sym / te / 1e9, decode=n_sym / td / 1e9)
+                       f"the C oracle on {threads} host threads (nproc {nproc}, {usable} usable "
+                       f"by this job): enc {n_sym / te / 1e9:.4f} Gsym/s, dec "
+                       f"{n_sym / td / 1e9:.4f} Gsym/s",
+                encode=n_sym / te / 1e9, decode=n_sym / td / 1e9,
+                single_core=dict(value=S1 * L / (te1 + td1) / 1e9, encode=S1 * L / te1 / 1e9,
+                                 decode=S1 * L / td1 / 1e9, sample=f"{S1} chunks, 1 thread"))
+
+
+def resolve_world(args):
+    """(world, rank, local_rank) of this process.  With --gpus N > 1 and no WORLD_SIZE in the
+    environment, launch the N ranks (this process then only waits for them: it exits here)."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        n = args.gpus or 1
+        if n > 1:
+            import torch  # device_count() does not initialise the GPU
+            have = torch.cuda.device_count()
+            if have < n and os.environ.get("RC_BENCH_ONE_DEVICE") != "1":
+                sys.stderr.write(f"bench.py: --gpus {n} but {have} GPU(s) visible\n")
+                sys.exit(2)
+            from range_coder_rust_amd import shard
+            sys.exit(shard.launch_ranks(os.path.abspath(__file__), sys.argv[1:], n))
+        return 1, 0, 0
+    world = int(env_world)
+    if args.gpus is not None and args.gpus != world:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}\n")
+        sys.exit(2)
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
 def main():
     args = parse()
+    world, rank, local = resolve_world(args)
+    if args.config is None:
+        args.config = "zipf" if world > 1 else "uniform"
+    if args.global_chunks is None:
+        args.global_chunks = (1 << 20) if world > 1 else 0
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # RC_BENCH_ONE_DEVICE=1 (rehearsal of the N-rank path on a one-GPU box): every rank on
+    # device 0, control messages over gloo
+    global CTRL_DEVICE
+    one_dev = os.environ.get("RC_BENCH_ONE_DEVICE") == "1"
+    gpu = 0 if one_dev else local
+    torch.cuda.set_device(gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if one_dev:
+            dist.init_process_group("gloo")
+            CTRL_DEVICE = "cpu"
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
 
     import range_coder_rust_amd as rc
     from range_coder_rust_amd import synth
-    ctx = rc.default_context(local)
+    ctx = rc.default_context(gpu)
 
     from range_coder_rust_amd import shard
     L = args.chunk_bytes
@@ -327,7 +409,10 @@ def main():
     else:
         n = args.chunks
         lo, n_all, scaling = rank * n, n * world, "weak"
-    leg = Leg(torch, rc, synth, ctx, args.config, n, L, lo)
+    # N > 1 also runs the weak uniform load (2^20 chunks per rank): one arena for both legs
+    weak_n = args.chunks if (world > 1 and args.global_chunks and not args.no_zipf) else 0
+    bufs = Leg.alloc(torch, torch.device("cuda", gpu), max(n, weak_n), L)
+    leg = Leg(torch, rc, synth, ctx, args.config, n, L, lo, bufs=bufs)
     res = run_leg(torch, dist, leg, args.steps, args.warmup, world)
     n_sym_all = n_all * L
     value = n_sym_all * args.steps / res["t"] / 1e9
@@ -357,11 +442,23 @@ def main():
                     alg_bytes_per_launch=alg_bytes)
 
     extras = {}
+    if weak_n:
+        u = Leg(torch, rc, synth, ctx, "uniform", weak_n, L, rank * weak_n, bufs=bufs)
+        ur = run_leg(torch, dist, u, max(2, args.steps // 2), 1, world)
+        extras["uniform_weak"] = dict(
+            workload=f"configs[1] on every rank: {weak_n} x {L // 1024} KiB chunks per GPU, "
+                     f"uniform-256 static model (weak scaling)",
+            value=round(weak_n * world * L * max(2, args.steps // 2) / ur["t"] / 1e9, 3),
+            encode_gsym_s=round(weak_n * L / ur["enc_ms"] / 1e6, 3),
+            decode_gsym_s=round(weak_n * L / ur["dec_ms"] / 1e6, 3),
+            bit_exact_round_trip=ur["ok"])
     if not args.no_zipf and args.config == "uniform":
-        z = Leg(torch, rc, synth, ctx, "zipf", n, L, lo, bufs=leg.bufs)
+        z = Leg(torch, rc, synth, ctx, "zipf", n, L, lo, bufs=bufs)
         zr = run_leg(torch, dist, z, max(2, args.steps // 2), 1, world)
         zb = n * L + zr["code_bytes"]
         extras["zipf1.2"] = dict(
+            workload=f"configs[2] (and configs[4] at N = {world}): {n} x {L // 1024} KiB chunks "
+                     f"per GPU, Zipf(1.2) static model",
             value=round(n_sym_all * max(2, args.steps // 2) / zr["t"] / 1e9, 3),
             encode_gsym_s=round(n * L / zr["enc_ms"] / 1e6, 3),
             decode_gsym_s=round(n * L / zr["dec_ms"] / 1e6, 3),
@@ -379,7 +476,7 @@ def main():
     if not args.no_adaptive and args.config == "uniform" and L % 16384 == 0:
         La = 16384
         na = n * (L // La)
-        a = Leg(torch, rc, synth, ctx, "adaptive", na, La, lo * (L // La), bufs=leg.bufs)
+        a = Leg(torch, rc, synth, ctx, "adaptive", na, La, lo * (L // La), bufs=bufs)
         ar = run_leg(torch, dist, a, max(2, args.steps // 2), 1, world)
         extras["adaptive_c4"] = dict(
             workload=f"configs[3]: {na} x 16 KiB chunks per GPU, adaptive order-0 "
@@ -390,17 +487,18 @@ def main():
             encode_ms=round(ar["enc_ms"], 3), decode_ms=round(ar["dec_ms"], 3),
             bytes_per_symbol=round(ar["code_bytes"] / (na * La), 5),
             bit_exact_round_trip=ar["ok"])
-    if extras:
-        # restore the headline inputs for the CPU baseline sample
-        synth.fill(ctx, leg.seed, leg.inv, leg.syms, L, n)
-        leg.encode()
-        torch.cuda.synchronize()
 
     cpu_b = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        cpu_b = cpu_baseline(torch, leg, args.cpu_seconds, threads)
+        if extras:
+            # restore the headline inputs and code for the CPU baseline sample
+            synth.fill(ctx, leg.seed, leg.inv, leg.syms, L, n)
+            leg.encode()
+            torch.cuda.synchronize()
+        cpu_b = cpu_baseline(torch, leg, args.cpu_seconds, args.cpu_threads)
 
+    ok_all = res["ok"] and all(e.get("bit_exact_round_trip", True) for e in extras.values()
+                               if isinstance(e, dict))
     if rank == 0:
         model = ("uniform-256 static (c=1, total=256)" if args.config == "uniform"
                  else "Zipf(1.2) static (total 2^16)")
@@ -438,7 +536,7 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    if not res["ok"]:
+    if not ok_all:
         sys.exit(3)
 
 

@@ -53,6 +53,16 @@ typedef int rc_status;
                               (decoder.rs:33, pop_front().unwrap())                         */
 #define RC_F_CORRUPT 16u   /* decoder selected a c_freq == 0 symbol (only possible on corrupt
                               input): the reference loops forever                            */
+#define RC_F_TOO_LONG 32u  /* chunk of more than RC_MAX_CHUNK_SYMBOLS symbols: the batch kernels
+                              keep 32-bit in-chunk stream positions, so such a chunk is neither
+                              read nor written (out_len 0).  The reference has no limit
+                              (VecDeque, encoder.rs:7-11): code a longer stream with the
+                              resumable stream entry points (rc_stream_*), which have none    */
+
+/* Longest chunk of the batch entry points.  A symbol settles at most 12 code bytes (5 in
+ * no_carry_expansion, range_coder.rs:110-116, and 7 in range_reduction_expansion, :126-135;
+ * DESIGN.md §3), so 2^25 symbols stay below 2^29 code bytes = 2^32 bits. */
+#define RC_MAX_CHUNK_SYMBOLS (1ull << 25)
 
 /* Maximum chunks per batch call (grid limit) */
 #define RC_MAX_CHUNKS (1u << 28)

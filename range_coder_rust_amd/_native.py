@@ -21,6 +21,8 @@ F_BAD_SYMBOL = 2
 F_CAPACITY = 4
 F_TRUNCATED = 8
 F_CORRUPT = 16
+F_TOO_LONG = 32
+MAX_CHUNK_SYMBOLS = 1 << 25  # RC_MAX_CHUNK_SYMBOLS
 
 # every symbol include/range_coder.h declares (checked by tests/test_abi.py)
 EXPORTS = (

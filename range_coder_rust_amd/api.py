@@ -26,7 +26,7 @@ from . import _native as N
 __all__ = [
     "Context", "StaticModel", "PModel", "FreqTable", "Encoder", "Decoder", "RangeCoderError",
     "ZeroFrequencyError", "BadSymbolError", "TruncatedStreamError", "CorruptStreamError",
-    "CapacityError", "encode_batch", "decode_batch", "encode_chunks", "decode_chunks",
+    "CapacityError", "ChunkTooLongError", "encode_batch", "decode_batch", "encode_chunks", "decode_chunks",
     "default_context", "flag_names", "slot_capacity",
 ]
 
@@ -56,16 +56,21 @@ class CapacityError(RangeCoderError):
     """An encoded chunk did not fit its output slot."""
 
 
+class ChunkTooLongError(RangeCoderError):
+    """A batch chunk of more than RC_MAX_CHUNK_SYMBOLS (2^25) symbols (32-bit in-chunk stream
+    positions; the stream API -- Encoder / Decoder -- has no such limit)."""
+
+
 _FLAG_ERRORS = [
     (N.F_ZERO_FREQ, ZeroFrequencyError), (N.F_BAD_SYMBOL, BadSymbolError),
     (N.F_CAPACITY, CapacityError), (N.F_TRUNCATED, TruncatedStreamError),
-    (N.F_CORRUPT, CorruptStreamError),
+    (N.F_CORRUPT, CorruptStreamError), (N.F_TOO_LONG, ChunkTooLongError),
 ]
 
 
 def flag_names(f):
     names = {N.F_ZERO_FREQ: "ZERO_FREQ", N.F_BAD_SYMBOL: "BAD_SYMBOL", N.F_CAPACITY: "CAPACITY",
-             N.F_TRUNCATED: "TRUNCATED", N.F_CORRUPT: "CORRUPT"}
+             N.F_TRUNCATED: "TRUNCATED", N.F_CORRUPT: "CORRUPT", N.F_TOO_LONG: "TOO_LONG"}
     return [v for k, v in names.items() if f & k]
 
 
@@ -374,6 +379,10 @@ def encode_chunks(model, chunks, raise_on_error=True):
     if n == 0:
         return []
     lens = np.array([len(a) for a in arrs], dtype=np.int64)
+    if int(lens.max()) > N.MAX_CHUNK_SYMBOLS:
+        raise ChunkTooLongError(f"chunk of {int(lens.max())} symbols: the batch API takes at "
+                                f"most {N.MAX_CHUNK_SYMBOLS} per chunk (use Encoder for longer "
+                                f"streams)")
     sym_off = np.zeros(n + 1, dtype=np.int64)
     sym_off[1:] = np.cumsum(lens)
     bits = model.max_bits_per_symbol()
@@ -414,6 +423,10 @@ def decode_chunks(model, codes, counts, raise_on_error=True):
     coff = np.zeros(n, dtype=np.int64)
     coff[1:] = np.cumsum(clen)[:-1]
     counts = np.asarray(counts, dtype=np.int64)
+    if int(counts.max()) > N.MAX_CHUNK_SYMBOLS:
+        raise ChunkTooLongError(f"chunk of {int(counts.max())} symbols: the batch API takes at "
+                                f"most {N.MAX_CHUNK_SYMBOLS} per chunk (use Decoder for longer "
+                                f"streams)")
     sym_off = np.zeros(n + 1, dtype=np.int64)
     sym_off[1:] = np.cumsum(counts)
     blob = np.frombuffer(b"".join(codes) + b"\0" * 16, dtype=np.uint8)

@@ -531,7 +531,7 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const u32 lane = threadIdx.x & 63u;
   const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 k = blockIdx.x * 64 + lane;
-  const bool live = k < n_chunks;
+  bool live = k < n_chunks;
   RC_VGPR_FLOOR_128();
   u64 n = 0, cap = 0;
   const uint8_t* sp = syms;
@@ -542,6 +542,14 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     sp = syms + a;
     lo = out + b;
     cap = out_off[k + 1] - b;
+  }
+  if (n > RC_MAX_CHUNK_SYMBOLS) {  // 32-bit stream positions (include/range_coder.h)
+    if (wave == 1) {
+      out_len[k] = 0;
+      flags[k] = RC_F_TOO_LONG;
+    }
+    live = false;
+    n = 0;
   }
   // 8-symbol steps: the same count in both waves (they hold the same 64 chunks)
   const u32 T = __builtin_amdgcn_readfirstlane(wave_max(live ? (u32)((n + 7) >> 3) : 0u));
@@ -845,9 +853,12 @@ __global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     n = sym_off[L.k + 1] - a;
     L.op = syms_out + a;
   }
-  const bool trunc0 = live && L.clen < 8;  // Decoder::new panics (decoder.rs:21)
+  const bool too_long = live && n > RC_MAX_CHUNK_SYMBOLS;  // 32-bit stream positions
+  const bool trunc0 = live && !too_long && L.clen < 8;  // Decoder::new panics (decoder.rs:21)
+  if (too_long) flags[L.k] = RC_F_TOO_LONG;
   if (trunc0) flags[L.k] = RC_F_TRUNCATED;
-  L.done = !live || trunc0;
+  L.done = !live || trunc0 || too_long;
+  if (L.done) n = 0;
   // lane L's u16 at byte 4 (L mod 32) + 2 (L div 32) of each row: a ds_read_u16 / ds_write_b16
   // serves lanes 0-31 and 32-63 as separate groups, and within a group every lane has its own
   // bank (lane pairs sharing a dword conflicted 2-way whenever they read different rows)

@@ -261,6 +261,12 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
     o0 = out_off[k];
     o1 = out_off[k + 1];
   }
+  // B (bit position) is 32-bit: a longer chunk is flagged, not read, and its slot not written
+  const bool too_long = n > RC_MAX_CHUNK_SYMBOLS;
+  if (too_long) {
+    n = 0;
+    o1 = o0;
+  }
   const u32 a = (u32)(((uintptr_t)out + o0) & (ENC_UNIT - 1));
   u64 cap = o1 - o0;
   if (cap > 0xFFFFFF00ull - a) cap = 0xFFFFFF00ull - a;
@@ -362,8 +368,8 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   if (live) {
     if (SM == 1) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
     if (!e.err && (u64)len > cap) e.err = RC_F_CAPACITY;
-    out_len[k] = len;
-    flags[k] = e.err;
+    out_len[k] = too_long ? 0u : len;
+    flags[k] = too_long ? RC_F_TOO_LONG : e.err;
   }
 }
 

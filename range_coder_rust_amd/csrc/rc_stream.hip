@@ -240,9 +240,12 @@ rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   for (u32 k = 0; k < n_chunks; ++k)
     if (sym_off[k + 1] < sym_off[k] || out_off[k + 1] < out_off[k]) return RC_E_ARG;
   DevSet g(dev);
+  // a chunk the kernel flags RC_F_TOO_LONG (never read nor written) is staged as empty
+  auto too_long = [&](u32 k) { return sym_off[k + 1] - sym_off[k] > RC_MAX_CHUNK_SYMBOLS; };
   const std::vector<Batch> bs = plan(
-      n_chunks, [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = sym_off[k + 1]; },
-      [&](u32 k, u64& a, u64& b) { a = out_off[k], b = out_off[k + 1]; });
+      n_chunks,
+      [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = too_long(k) ? a : sym_off[k + 1]; },
+      [&](u32 k, u64& a, u64& b) { a = out_off[k], b = too_long(k) ? a : out_off[k + 1]; });
   size_t in_max = 0, out_max = 0, n_off = 0;
   u32 kmax = 0;
   for (const Batch& b : bs) {
@@ -306,9 +309,11 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   for (u32 k = 0; k < n_chunks; ++k)
     if (sym_off[k + 1] < sym_off[k]) return RC_E_ARG;
   DevSet g(dev);
+  auto too_long = [&](u32 k) { return sym_off[k + 1] - sym_off[k] > RC_MAX_CHUNK_SYMBOLS; };
   const std::vector<Batch> bs = plan(
-      n_chunks, [&](u32 k, u64& a, u64& b) { a = code_off[k], b = code_off[k] + code_len[k]; },
-      [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = sym_off[k + 1]; });
+      n_chunks,
+      [&](u32 k, u64& a, u64& b) { a = code_off[k], b = too_long(k) ? a : a + code_len[k]; },
+      [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = too_long(k) ? a : sym_off[k + 1]; });
   size_t in_max = 0, out_max = 0, n_off = 0;
   u32 kmax = 0;
   u64 cmin = ~0ull, cmax = 0;

@@ -62,3 +62,38 @@ def max_over_ranks(value, dist=None, device=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_ranks_true(flag, dist=None, device=None):
+    """True when `flag` holds on every rank (an all-reduce MIN of one int)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return bool(flag)
+    import torch
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def free_port():
+    """A free TCP port on 127.0.0.1 for the rendezvous."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(script, argv, nprocs, port=None, env=None):
+    """Run `script argv` as `nprocs` rank processes of one node (one per GPU) under
+    torch.distributed.run with a 127.0.0.1 rendezvous, and return its exit code.
+
+    The caller must not have initialised the GPU (no HIP call, no torch.cuda.is_available()):
+    the ranks are fresh child processes, never an exec of this one.  Each rank reads RANK,
+    LOCAL_RANK and WORLD_SIZE from its environment."""
+    import subprocess
+    import sys
+    if nprocs < 1:
+        raise ValueError(f"nprocs must be >= 1, got {nprocs}")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={int(nprocs)}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port or free_port()), script] + list(argv)
+    return subprocess.run(cmd, env=env).returncode

@@ -4,7 +4,6 @@ The multi-process case runs world_size 2 on gloo (CPU) with the C oracle as the 
 and checks that the ranks' concatenated code equals a single-process encode of all chunks."""
 import multiprocessing as mp
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -83,17 +82,11 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def test_two_rank_gloo_shards_equal_single_process():
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    port = shard.free_port()
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
