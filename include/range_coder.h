@@ -53,6 +53,11 @@ typedef int rc_status;
                               (decoder.rs:33, pop_front().unwrap())                         */
 #define RC_F_CORRUPT 16u   /* decoder selected a c_freq == 0 symbol (only possible on corrupt
                               input): the reference loops forever                            */
+#define RC_F_BAD_MODEL 64u /* stream API: a (c, cum, total) on which the reference panics — total
+                              0 (u64 division by zero, range_coder.rs:38-40), LowerBoundOverflow
+                              (:68-81) or UpperBoundOverflow (upper_bound().unwrap(), :138-146) */
+#define RC_F_FINISHED 128u /* stream API: encode after Encoder::finish, which consumes the
+                              encoder (encoder.rs:40)                                        */
 #define RC_F_TOO_LONG 32u  /* chunk of more than RC_MAX_CHUNK_SYMBOLS symbols: the batch kernels
                               keep 32-bit in-chunk stream positions, so such a chunk is neither
                               read nor written (out_len 0).  The reference has no limit
@@ -142,6 +147,73 @@ rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
 rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
                          const uint64_t* code_off, const uint64_t* code_len, uint8_t* syms_out,
                          const uint64_t* sym_off, uint32_t n_chunks, uint32_t* flags);
+
+/* ---- resumable streams: the reference's per-call Encoder / Decoder (any PModel) ----
+ * The batch entry points code whole chunks against one table.  The reference instead reads the
+ * model on EVERY call — Encoder::encode takes (c_freq(i), cum_freq(i), total_freq()) of the
+ * caller's PModel at that moment (encoder.rs:24-31), Decoder::decode runs find_index and reads
+ * the table again (decoder.rs:38-50) — so a caller may change its model between calls
+ * (adaptive models).  These entry points keep a stream's state between calls instead:
+ *   encode: the caller passes the (c, cum, total) triple it read for each symbol;
+ *   decode: the caller passes the table to use for the next n symbols (FreqTable::find_index's
+ *           binary search over cum, sample_impl.rs:27-45, and param_update over (c, cum, total),
+ *           evaluated as given: no consistency requirement on the table).
+ * State positions are 64-bit: a stream has no length limit.  Per-symbol arithmetic follows
+ * range_coder.rs:53-135 exactly; where the reference panics or never terminates the stream is
+ * flagged (sticky) and stops before that symbol. */
+typedef struct rc_stream_state {
+  uint64_t lower_bound, range; /* RangeCoder (range_coder.rs:7-12): Encoder::range_coder, or
+                                  Decoder::range_coder() (decoder.rs:24-26)                   */
+  uint64_t data;               /* decoder: Decoder::data() (decoder.rs:27-29)                */
+  uint64_t pos;                /* encoder: code bytes emitted (peek_code().len(), encoder.rs:18);
+                                  decoder: code bytes consumed, incl. the 8 of Decoder::new   */
+  uint64_t n;                  /* symbols coded so far                                       */
+  uint32_t flags;              /* sticky RC_F_* (ZERO_FREQ, BAD_MODEL, TRUNCATED, CORRUPT,
+                                  FINISHED)                                                  */
+  uint32_t stage;              /* 0 fresh (a decoder runs Decoder::new on its first call),
+                                  1 running, 2 finished (encoder)                            */
+} rc_stream_state;
+/* RangeCoder::default / Encoder::new / a decoder before Decoder::new */
+#define RC_STREAM_STATE_INIT {0u, ~(uint64_t)0, 0u, 0u, 0u, 0u, 0u}
+/* bytes one call may emit: a symbol settles at most 12 bytes, finish 8 */
+#define RC_STREAM_MAX_BYTES(n, finish) (12ull * (uint64_t)(n) + ((finish) ? 8ull : 0ull))
+
+/* Encoder::encode x n (+ Encoder::finish if `finish`) for n_streams independent streams.
+ * states_dev     n_streams rc_stream_state, updated in place
+ * triples_dev    per symbol {c_freq, cum_freq, total_freq} (3 x uint32); stream k's symbols are
+ *                triples [sym_off[k], sym_off[k+1])
+ * out_dev        this call's NEW bytes of stream k go to out[out_off[k] ..); the slot must hold
+ *                RC_STREAM_MAX_BYTES(symbols, finish) or the stream is flagged RC_F_CAPACITY
+ *                (not sticky) and left unchanged
+ * out_len_dev    n_streams: new bytes written
+ * nbytes_dev     NULL or one uint8 per symbol (same indexing as the triples): encode()'s return
+ *                value, the bytes that symbol settled (encoder.rs:34-36)
+ * flags_dev      n_streams: RC_F_* of this call (the sticky ones are also in the state)      */
+rc_status rc_stream_encode(rc_ctx* ctx, rc_stream_state* states_dev, const uint32_t* triples_dev,
+                           const uint64_t* sym_off_dev, uint32_t n_streams, uint8_t* out_dev,
+                           const uint64_t* out_off_dev, uint64_t* out_len_dev,
+                           uint8_t* nbytes_dev, uint32_t finish, uint32_t* flags_dev);
+/* Decoder::decode x (sym_off[k+1] - sym_off[k]) for n_streams streams against one table
+ * (c_dev, cum_dev: n_symbols uint32 each; total_freq).  Stream k's whole code is
+ * code[code_off[k] .. + code_len[k]) and the state's pos indexes it.  Symbols go to
+ * syms_dev[sym_off[k] ..).  A stream stops before its first failing symbol; state.n counts the
+ * symbols decoded.                                                                           */
+rc_status rc_stream_decode(rc_ctx* ctx, const uint32_t* c_dev, const uint32_t* cum_dev,
+                           uint32_t n_symbols, uint32_t total_freq, rc_stream_state* states_dev,
+                           const uint8_t* code_dev, const uint64_t* code_off_dev,
+                           const uint64_t* code_len_dev, uint8_t* syms_dev,
+                           const uint64_t* sym_off_dev, uint32_t n_streams, uint32_t* flags_dev);
+/* One stream in host memory, synchronous (the host mirrors' Encoder / Decoder).  Only the bytes a
+ * call can touch cross PCIe: the encoder's new bytes, the decoder's window
+ * [pos, pos + RC_STREAM_MAX_BYTES(n, 0) + 8).  Return RC_E_CHUNK when a flag is set (in
+ * *flags_out, and sticky ones in the state).                                                 */
+rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint32_t* triples,
+                                uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
+                                uint8_t* nbytes, uint32_t finish, uint32_t* flags_out);
+rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* cum,
+                                uint32_t n_symbols, uint32_t total_freq, rc_stream_state* state,
+                                const uint8_t* code, uint64_t code_len, uint8_t* syms,
+                                uint64_t n, uint32_t* flags_out);
 
 /* ---- synthetic workload generator (bench/test inputs, generated in HBM) ----
  * Fills n_chunks chunks of chunk_len symbols at syms_dev (chunk k at k*chunk_len).  Symbol i of

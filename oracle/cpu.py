@@ -21,6 +21,21 @@ F_BAD_SYMBOL = 2
 F_CAPACITY = 4
 F_TRUNCATED = 8
 F_CORRUPT = 16
+F_BAD_MODEL = 64
+F_FINISHED = 128
+
+
+class Stream(ctypes.Structure):
+    """orc_stream (rc_oracle.h) == rc_stream_state (include/range_coder.h)."""
+    _fields_ = [(n, _U64) for n in ("lower_bound", "range", "data", "pos", "n")] + \
+               [("flags", _U32), ("stage", _U32)]
+
+    @classmethod
+    def fresh(cls):
+        return cls(0, (1 << 64) - 1, 0, 0, 0, 0, 0)
+
+    def tuple(self):
+        return (self.lower_bound, self.range, self.data, self.pos, self.n, self.flags, self.stage)
 
 
 def build():
@@ -47,6 +62,12 @@ def lib():
         L.orc_encode_adaptive.restype = _U32
         L.orc_decode_adaptive.argtypes = [_U32, _U32, _U32, _U32, _P, _U64, _U64, _P]
         L.orc_decode_adaptive.restype = _U32
+        L.orc_stream_encode.argtypes = [ctypes.POINTER(Stream), _P, _U64, _P, _U64,
+                                        ctypes.POINTER(_U64), _P, ctypes.c_int]
+        L.orc_stream_encode.restype = _U32
+        L.orc_stream_decode.argtypes = [ctypes.POINTER(Stream), _P, _P, _U32, _U32, _P, _U64, _P,
+                                        _U64, ctypes.POINTER(_U64)]
+        L.orc_stream_decode.restype = _U32
         L.orc_fnv1a64.argtypes = [_P, _U64]
         L.orc_fnv1a64.restype = _U64
         _LIB = L
@@ -140,3 +161,29 @@ def decode_adaptive(n_alpha, inc, limit, period, code, n):
 def fnv1a64(b):
     a = _u8(b)
     return int(lib().orc_fnv1a64(_ptr(a), len(a)))
+
+
+def stream_encode(st, triples, finish=False, cap=None):
+    """orc_stream_encode: st (Stream) advances; returns (flags, new bytes, per-symbol counts)."""
+    t = np.ascontiguousarray(triples, dtype=np.uint32).reshape(-1)
+    n = t.size // 3
+    if cap is None:
+        cap = 12 * n + (8 if finish else 0)
+    out = np.zeros(max(cap, 1), np.uint8)
+    nb = np.zeros(max(n, 1), np.uint8)
+    ol = _U64()
+    n0 = st.n
+    f = lib().orc_stream_encode(ctypes.byref(st), _ptr(t), n, _ptr(out), cap, ctypes.byref(ol),
+                                _ptr(nb), 1 if finish else 0)
+    return int(f), bytes(out[: ol.value]), nb[: st.n - n0].copy()
+
+
+def stream_decode(st, c, cum, total, code, n):
+    """orc_stream_decode over the whole code: returns (flags, decoded symbols)."""
+    c, cum = _table(c, cum)
+    code = _u8(code)
+    out = np.zeros(max(n, 1), np.uint8)
+    done = _U64()
+    f = lib().orc_stream_decode(ctypes.byref(st), _ptr(c), _ptr(cum), len(c), total, _ptr(code),
+                                len(code), _ptr(out), n, ctypes.byref(done))
+    return int(f), out[: done.value].copy()

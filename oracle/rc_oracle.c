@@ -259,3 +259,110 @@ void orc_decode_batch(const uint32_t* c, const uint32_t* cum, uint32_t n_alpha, 
     j.flags = flags; j.n_chunks = n_chunks;
     run_batch(&j, threads);
 }
+
+/* ---------------- resumable single streams (rc_stream_* restated) ---------------- */
+void orc_stream_init(orc_stream* st) {
+    memset(st, 0, sizeof *st);
+    st->range = UINT64_MAX; /* RangeCoder::default, range_coder.rs:13-20 */
+}
+
+/* RangeCoder::param_update (range_coder.rs:53-92) with the reference's panics as flags:
+ * returns the settled byte count, or -(flag) */
+static int param_update_checked(orc_range_coder* rc, uint32_t c_freq, uint32_t cum_freq,
+                                uint32_t total_freq, uint8_t out[16], uint32_t zero_flag) {
+    if (total_freq == 0) return -(int)ORC_F_BAD_MODEL;   /* u64 / 0 panics (:38-40) */
+    uint64_t r = rc->range / (uint64_t)total_freq;
+    uint64_t range = r * (uint64_t)c_freq;                /* :65 (release: wraps) */
+    uint64_t add = r * (uint64_t)cum_freq;
+    if (rc->lower_bound + add < add) return -(int)ORC_F_BAD_MODEL; /* overflowing_add, :68-81 */
+    uint64_t low = rc->lower_bound + add;
+    if (range == 0) return -(int)zero_flag;               /* :83-85 never terminates */
+    if (low + range < range) return -(int)ORC_F_BAD_MODEL; /* upper_bound().unwrap(), :138-146 */
+    rc->range = range;
+    rc->lower_bound = low;
+    int n = 0;
+    for (;;) { /* no_carry_expansion, :110-116 (upper_bound cannot overflow from here on) */
+        if ((rc->lower_bound ^ (rc->lower_bound + rc->range)) < TOP8)
+            out[n++] = left_shift(rc);
+        else
+            break;
+    }
+    while (rc->range < TOP16) { /* range_reduction_expansion, :126-135 */
+        rc->range = ~rc->lower_bound & (TOP16 - 1);
+        out[n++] = left_shift(rc);
+    }
+    return n;
+}
+
+uint32_t orc_stream_encode(orc_stream* st, const uint32_t* triples, uint64_t n, uint8_t* out,
+                           uint64_t cap, uint64_t* out_len, uint8_t* nbytes, int finish) {
+    uint64_t len = 0;
+    *out_len = 0;
+    if (st->flags) return st->flags;
+    if (st->stage == 2) return st->flags = ORC_F_FINISHED; /* finish() consumed the encoder */
+    if (cap < 12 * n + (finish ? 8 : 0)) return ORC_F_CAPACITY; /* not sticky, no change */
+    orc_range_coder rc = {st->lower_bound, st->range};
+    uint8_t tmp[16];
+    for (uint64_t i = 0; i < n; ++i) { /* Encoder::encode, encoder.rs:24-37 */
+        const uint32_t* t = triples + 3 * i;
+        orc_range_coder save = rc;
+        int k = param_update_checked(&rc, t[0], t[1], t[2], tmp, ORC_F_ZERO_FREQ);
+        if (k < 0) {
+            rc = save;
+            st->flags = (uint32_t)(-k);
+            break;
+        }
+        for (int j = 0; j < k; ++j) out[len++] = tmp[j];
+        if (nbytes) nbytes[i] = (uint8_t)k;
+        st->n++;
+    }
+    if (finish && !st->flags) { /* Encoder::finish, encoder.rs:40-46 */
+        for (int j = 0; j < 8; ++j) out[len++] = left_shift(&rc);
+        st->stage = 2;
+    } else if (st->stage == 0) {
+        st->stage = 1;
+    }
+    st->lower_bound = rc.lower_bound;
+    st->range = rc.range;
+    st->pos += len;
+    *out_len = len;
+    return st->flags;
+}
+
+uint32_t orc_stream_decode(orc_stream* st, const uint32_t* c, const uint32_t* cum,
+                           uint32_t n_alpha, uint32_t total, const uint8_t* code,
+                           uint64_t code_len, uint8_t* syms, uint64_t n, uint64_t* n_done) {
+    *n_done = 0;
+    if (st->flags) return st->flags;
+    if (st->stage == 0) { /* Decoder::new, decoder.rs:14-23 */
+        if (code_len < 8) return st->flags = ORC_F_TRUNCATED;
+        st->data = 0;
+        for (st->pos = 0; st->pos < 8; ++st->pos) st->data = (st->data << 8) | code[st->pos];
+        st->stage = 1;
+    }
+    orc_range_coder rc = {st->lower_bound, st->range};
+    uint8_t tmp[16];
+    for (uint64_t i = 0; i < n; ++i) { /* Decoder::decode, decoder.rs:38-54 */
+        if (total == 0) { st->flags = ORC_F_BAD_MODEL; break; } /* find_index's division */
+        uint32_t s = find_index(cum, n_alpha, total, &rc, st->data);
+        orc_range_coder save = rc;
+        int k = param_update_checked(&rc, c[s], cum[s], total, tmp, ORC_F_CORRUPT);
+        if (k < 0) {
+            rc = save;
+            st->flags = (uint32_t)(-k);
+            break;
+        }
+        if (st->pos + (uint64_t)k > code_len) { /* shift_left_buffer panics, :31-35 */
+            rc = save;
+            st->flags = ORC_F_TRUNCATED;
+            break;
+        }
+        for (int j = 0; j < k; ++j) st->data = (st->data << 8) | code[st->pos++];
+        syms[i] = (uint8_t)s;
+        st->n++;
+        *n_done = i + 1;
+    }
+    st->lower_bound = rc.lower_bound;
+    st->range = rc.range;
+    return st->flags;
+}

@@ -27,6 +27,10 @@ extern "C" {
 #define ORC_F_CAPACITY   4u  /* encoded stream longer than its output slot */
 #define ORC_F_TRUNCATED  8u  /* decoder ran out of code bytes: reference panics (decoder.rs:33) */
 #define ORC_F_CORRUPT   16u  /* decoder selected a c==0 symbol: reference loops forever */
+#define ORC_F_BAD_MODEL 64u  /* (c, cum, total) on which the reference panics: total == 0
+                                (division by zero, range_coder.rs:38-40), LowerBoundOverflow
+                                (:68-81) or UpperBoundOverflow (:138-146) */
+#define ORC_F_FINISHED 128u  /* encode after Encoder::finish (which consumes it, encoder.rs:40) */
 
 typedef struct orc_range_coder {
     uint64_t lower_bound; /* range_coder.rs:9  */
@@ -70,6 +74,33 @@ uint32_t orc_encode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit, uin
                              uint64_t* out_len);
 uint32_t orc_decode_adaptive(uint32_t n_alpha, uint32_t inc, uint32_t limit, uint32_t period,
                              const uint8_t* code, uint64_t code_len, uint64_t n, uint8_t* syms_out);
+
+/* Resumable single streams (the rc_stream_* entry points of include/range_coder.h): the state of
+ * one reference Encoder or Decoder between calls.  stage: 0 fresh (a decoder has not yet run
+ * Decoder::new), 1 running, 2 finished (encoder).  flags: sticky first error. */
+typedef struct orc_stream {
+    uint64_t lower_bound, range; /* RangeCoder (range_coder.rs:7-12) */
+    uint64_t data;               /* Decoder::data (decoder.rs:8) */
+    uint64_t pos;                /* encoder: bytes emitted; decoder: bytes consumed */
+    uint64_t n;                  /* symbols coded */
+    uint32_t flags, stage;
+} orc_stream;
+
+void orc_stream_init(orc_stream* st);
+/* n x Encoder::encode with the (c_freq, cum_freq, total_freq) triple read per call
+ * (encoder.rs:24-37), then Encoder::finish if `finish` (encoder.rs:40-46).  New bytes go to
+ * out[0..); *out_len = their count; nbytes[i] = the return value of the i-th encode().  The
+ * state advances over the symbols coded before an error.  cap < 12 n (+ 8 with finish):
+ * ORC_F_CAPACITY, nothing done.  Returns the flags. */
+uint32_t orc_stream_encode(orc_stream* st, const uint32_t* triples, uint64_t n, uint8_t* out,
+                           uint64_t cap, uint64_t* out_len, uint8_t* nbytes, int finish);
+/* Decoder::new (if fresh) + n x Decoder::decode (decoder.rs:14-54) with the sample
+ * FreqTable::find_index (sample_impl.rs:27-45) over an arbitrary (c, cum) table: code[0..code_len)
+ * is the whole stream (st->pos indexes it).  Stops before the first symbol that errs; *n_done
+ * symbols were written to syms.  Returns the flags. */
+uint32_t orc_stream_decode(orc_stream* st, const uint32_t* c, const uint32_t* cum,
+                           uint32_t n_alpha, uint32_t total, const uint8_t* code,
+                           uint64_t code_len, uint8_t* syms, uint64_t n, uint64_t* n_done);
 
 /* FNV-1a 64 of a byte string (used by the known-answer tests). */
 uint64_t orc_fnv1a64(const uint8_t* p, uint64_t n);

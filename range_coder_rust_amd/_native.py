@@ -22,6 +22,8 @@ F_CAPACITY = 4
 F_TRUNCATED = 8
 F_CORRUPT = 16
 F_TOO_LONG = 32
+F_BAD_MODEL = 64
+F_FINISHED = 128
 MAX_CHUNK_SYMBOLS = 1 << 25  # RC_MAX_CHUNK_SYMBOLS
 
 # every symbol include/range_coder.h declares (checked by tests/test_abi.py)
@@ -32,6 +34,7 @@ EXPORTS = (
     "rc_model_create_adaptive", "rc_model_destroy", "rc_encode_batch", "rc_decode_batch", "rc_encode_host",
     "rc_decode_host", "rc_synth_fill", "rc_histogram", "rc_quantize_counts", "rc_ideal_bits",
     "rc_container_pack", "rc_container_info_parse", "rc_container_offsets",
+    "rc_stream_encode", "rc_stream_decode", "rc_stream_encode_host", "rc_stream_decode_host",
 )
 RC_E_BAD_CONTAINER = -6
 RC_E_CAPACITY = -7
@@ -45,6 +48,20 @@ class ContainerInfo(ctypes.Structure):
                [(n, ctypes.c_uint64) for n in ("n_chunks", "n_syms", "payload_bytes", "table_off",
                                               "index_off", "payload_off", "container_bytes")]
 Q_ALL_SYMBOLS = 1
+
+
+class StreamState(ctypes.Structure):
+    """rc_stream_state (include/range_coder.h): one reference Encoder / Decoder between calls."""
+    _fields_ = [(n, ctypes.c_uint64) for n in ("lower_bound", "range", "data", "pos", "n")] + \
+               [("flags", ctypes.c_uint32), ("stage", ctypes.c_uint32)]
+
+    @classmethod
+    def fresh(cls):  # RC_STREAM_STATE_INIT
+        return cls(0, (1 << 64) - 1, 0, 0, 0, 0, 0)
+
+
+def stream_max_bytes(n, finish):  # RC_STREAM_MAX_BYTES
+    return 12 * int(n) + (8 if finish else 0)
 
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
@@ -95,6 +112,13 @@ def load():
     L.rc_container_pack.argtypes = [_P, _P, _P, _P, _P, _P, _U32, _P, _U64, ctypes.POINTER(_U64)]
     L.rc_container_info_parse.argtypes = [_P, _U64, ctypes.POINTER(ContainerInfo)]
     L.rc_container_offsets.argtypes = [_P, _P, ctypes.POINTER(ContainerInfo), _P, _P, _P]
+    SP = ctypes.POINTER(StreamState)
+    L.rc_stream_encode.argtypes = [_P, _P, _P, _P, _U32, _P, _P, _P, _P, _U32, _P]
+    L.rc_stream_decode.argtypes = [_P, _P, _P, _U32, _U32, _P, _P, _P, _P, _P, _P, _U32, _P]
+    L.rc_stream_encode_host.argtypes = [_P, SP, _P, _U64, _P, _U64, ctypes.POINTER(_U64), _P,
+                                        _U32, ctypes.POINTER(_U32)]
+    L.rc_stream_decode_host.argtypes = [_P, _P, _P, _U32, _U32, SP, _P, _U64, _P, _U64,
+                                        ctypes.POINTER(_U32)]
     for name in EXPORTS:
         if name not in ("rc_status_string", "rc_last_error"):
             getattr(L, name).restype = _I

@@ -26,7 +26,8 @@ from . import _native as N
 __all__ = [
     "Context", "StaticModel", "PModel", "FreqTable", "Encoder", "Decoder", "RangeCoderError",
     "ZeroFrequencyError", "BadSymbolError", "TruncatedStreamError", "CorruptStreamError",
-    "CapacityError", "ChunkTooLongError", "encode_batch", "decode_batch", "encode_chunks", "decode_chunks",
+    "CapacityError", "ChunkTooLongError", "BadModelError", "FinishedError", "RangeCoder",
+    "ByteCount", "stream_states", "stream_encode_batch", "stream_decode_batch", "encode_batch", "decode_batch", "encode_chunks", "decode_chunks",
     "default_context", "flag_names", "slot_capacity",
 ]
 
@@ -56,6 +57,16 @@ class CapacityError(RangeCoderError):
     """An encoded chunk did not fit its output slot."""
 
 
+class BadModelError(RangeCoderError):
+    """A (c_freq, cum_freq, total_freq) on which the reference panics: total 0 (division by
+    zero, range_coder.rs:38-40), LowerBoundOverflow (:68-81) or UpperBoundOverflow
+    (upper_bound().unwrap(), :138-146)."""
+
+
+class FinishedError(RangeCoderError):
+    """encode() after finish(): Encoder::finish takes the encoder by value (encoder.rs:40)."""
+
+
 class ChunkTooLongError(RangeCoderError):
     """A batch chunk of more than RC_MAX_CHUNK_SYMBOLS (2^25) symbols (32-bit in-chunk stream
     positions; the stream API -- Encoder / Decoder -- has no such limit)."""
@@ -65,12 +76,14 @@ _FLAG_ERRORS = [
     (N.F_ZERO_FREQ, ZeroFrequencyError), (N.F_BAD_SYMBOL, BadSymbolError),
     (N.F_CAPACITY, CapacityError), (N.F_TRUNCATED, TruncatedStreamError),
     (N.F_CORRUPT, CorruptStreamError), (N.F_TOO_LONG, ChunkTooLongError),
+    (N.F_BAD_MODEL, BadModelError), (N.F_FINISHED, FinishedError),
 ]
 
 
 def flag_names(f):
     names = {N.F_ZERO_FREQ: "ZERO_FREQ", N.F_BAD_SYMBOL: "BAD_SYMBOL", N.F_CAPACITY: "CAPACITY",
-             N.F_TRUNCATED: "TRUNCATED", N.F_CORRUPT: "CORRUPT", N.F_TOO_LONG: "TOO_LONG"}
+             N.F_TRUNCATED: "TRUNCATED", N.F_CORRUPT: "CORRUPT", N.F_TOO_LONG: "TOO_LONG",
+             N.F_BAD_MODEL: "BAD_MODEL", N.F_FINISHED: "FINISHED"}
     return [v for k, v in names.items() if f & k]
 
 
@@ -225,8 +238,12 @@ class FreqTable(PModel):
     def total_freq(self):  # :24-26
         return self.total
 
-    def find_index(self, decoder):  # :27-45 — the GPU decoder implements this inverse itself
+    def find_index(self, decoder):  # :27-45 — evaluated by the GPU decoders themselves
         raise NotImplementedError("FreqTable.find_index runs inside the GPU decode kernel")
+
+    def _rc_table(self):
+        """(c, cum, total) as read through c_freq / cum_freq / total_freq (fast path)."""
+        return tuple(self.c), tuple(self.cum), self.total
 
 
 class StaticModel:
@@ -445,83 +462,378 @@ def decode_chunks(model, codes, counts, raise_on_error=True):
 
 
 # ----------------------------------------------------------------------------- stream API
-class Encoder:
-    """Encoder (src/encoder.rs:7-55) for ONE stream.
+M64 = (1 << 64) - 1
 
-    encode(pmodel, index) stages the symbol (it cannot return the per-symbol byte count the
-    reference returns, encoder.rs:36, because nothing is coded until finish()); finish()
-    encodes the whole stream on the GPU and returns its bytes (== the reference's
-    VecDeque<u8>).  All symbols of one stream must use the same static model."""
 
-    def __init__(self):
-        self._syms = []
-        self._model = None
+class RangeCoder:
+    """RangeCoder (src/range_coder.rs:7-146): the public accessors of one coder state.
+
+    A snapshot: a stream's state lives with its GPU call between calls (rc_stream_state), so
+    Encoder.range_coder and Decoder.range_coder() return a copy.  param_update / left_shift are
+    pub(crate) in the reference and run only inside the kernels."""
+
+    TOP8 = 1 << (64 - 8)  # range_coder.rs:23
+    TOP16 = 1 << (64 - 16)  # range_coder.rs:24
+
+    def __init__(self, lower_bound=0, range_=M64):  # Default (:13-20)
+        self._low, self._range = int(lower_bound), int(range_)
 
     @classmethod
-    def new(cls):
+    def new(cls):  # :26-28
         return cls()
 
-    def encode(self, pmodel, index):
-        if self._model is None:
-            self._model = pmodel
-        elif pmodel is not self._model:
-            raise RangeCoderError("one static model per staged stream")
-        self._syms.append(int(index))
+    def lower_bound(self):  # :30-32
+        return self._low
 
-    def peek_code(self):
-        raise RangeCoderError("peek_code: the stream is coded in finish() on the GPU")
+    def range(self):  # :33-35
+        return self._range
 
-    def finish(self):
-        if self._model is None:
-            # no symbols: the reference emits the 8 bytes of lower_bound == 0
-            return bytes(8)
-        m = _snapshot(self._model)
-        if any(s < 0 or s >= m.n_symbols for s in self._syms):
-            raise BadSymbolError("symbol index outside the alphabet")
-        return encode_chunks(m, [np.array(self._syms, dtype=np.uint8)])[0]
+    def range_par_total(self, total_freq):  # :38-40
+        if int(total_freq) == 0:
+            raise BadModelError("range_par_total: attempt to divide by zero")
+        return self._range // int(total_freq)
+
+    def upper_bound(self):  # :138-146
+        s = self._low + self._range
+        if s > M64:
+            raise RangeCoderError(f"UpperBoundOverflow {{ lower_bound: {self._low}, "
+                                  f"range: {self._range} }}")
+        return s
+
+    def __eq__(self, other):
+        return (isinstance(other, RangeCoder) and
+                (self._low, self._range) == (other._low, other._range))
+
+    def __repr__(self):
+        return f"RangeCoder(lower_bound={self._low:#x}, range={self._range:#x})"
+
+
+class ByteCount:
+    """The value Encoder.encode returns: the number of bytes that symbol settled
+    (encoder.rs:34-36).  Symbols are staged and coded on the GPU in batches, so the count is
+    known once the symbol is flushed: int(), comparisons and arithmetic flush on demand (one
+    launch for everything staged); code that ignores the value, as sample_impl.rs:96 does,
+    never waits for it."""
+
+    __slots__ = ("_enc", "_i")
+
+    def __init__(self, enc, i):
+        self._enc, self._i = enc, i
+
+    def __int__(self):
+        return self._enc._count(self._i)
+
+    __index__ = __int__
+
+    def __eq__(self, other):
+        return int(self) == other
+
+    def __ne__(self, other):
+        return int(self) != other
+
+    def __lt__(self, other):
+        return int(self) < other
+
+    def __le__(self, other):
+        return int(self) <= other
+
+    def __gt__(self, other):
+        return int(self) > other
+
+    def __ge__(self, other):
+        return int(self) >= other
+
+    def __hash__(self):
+        return hash(int(self))
+
+    def __add__(self, other):
+        return int(self) + other
+
+    __radd__ = __add__
+
+    def __repr__(self):
+        return repr(int(self))
+
+
+def _u32(v, what):
+    v = int(v)
+    if not 0 <= v <= 0xFFFFFFFF:
+        raise RangeCoderError(f"{what} = {v} is not a u32")
+    return v
+
+
+def _table_of(pmodel):
+    """(c, cum, total) of a PModel, read through c_freq / cum_freq / total_freq over its
+    alphabet, as the reference's decode reads them (decoder.rs:38-50, sample_impl.rs:27-45)."""
+    fast = getattr(pmodel, "_rc_table", None)
+    if fast is not None:
+        return fast()
+    n = pmodel.alphabet_count()
+    return (tuple(int(pmodel.c_freq(i)) for i in range(n)),
+            tuple(int(pmodel.cum_freq(i)) for i in range(n)), int(pmodel.total_freq()))
+
+
+class Encoder:
+    """Encoder (src/encoder.rs:7-55) for ONE stream, with the reference's per-call semantics.
+
+    encode(pmodel, index) reads (c_freq(index), cum_freq(index), total_freq()) at that call, as
+    encoder.rs:24-31 does, so a model the caller changes between calls (an adaptive PModel) is
+    coded exactly as the reference codes it.  The triples are staged and coded on the GPU by the
+    resumable stream kernel (rc_stream_encode_host) when a result is needed: peek_code(),
+    range_coder, finish(), the int value of encode()'s ByteCount, or every 2^20 symbols.  A
+    stream has no length limit.  Errors the reference panics on surface as RangeCoderError
+    subclasses at the call that flushes them; the encoder is then unusable, as after a panic."""
+
+    FLUSH_AT = 1 << 20
+
+    def __init__(self, ctx=None):
+        self._ctx = ctx
+        self._state = N.StreamState.fresh()
+        self._code = bytearray()
+        self._trip = []            # staged (c, cum, total), flat
+        self._counts = bytearray()  # encode() return values of the flushed symbols
+        self._staged0 = 0          # index of the first staged symbol
+        self._finished = False
+
+    @classmethod
+    def new(cls):  # encoder.rs:14-16
+        return cls()
+
+    def encode(self, pmodel, index):  # encoder.rs:24-37
+        if self._finished:
+            raise FinishedError("encode after finish")
+        c = _u32(pmodel.c_freq(index), "c_freq")
+        cum = _u32(pmodel.cum_freq(index), "cum_freq")
+        total = _u32(pmodel.total_freq(), "total_freq")
+        if c == 0:  # range_coder.rs:83-85 would never terminate
+            raise ZeroFrequencyError(f"encode({index}): c_freq == 0")
+        if total == 0:  # range_coder.rs:38-40 divides by zero
+            raise BadModelError(f"encode({index}): total_freq == 0")
+        self._trip += (c, cum, total)
+        i = self._staged0 + len(self._trip) // 3 - 1
+        if len(self._trip) >= 3 * self.FLUSH_AT:
+            self._flush()
+        return ByteCount(self, i)
+
+    def peek_code(self):  # encoder.rs:18-20: the bytes emitted so far
+        self._flush()
+        return bytes(self._code)
+
+    @property
+    def range_coder(self):  # the pub field of encoder.rs:8 (a snapshot)
+        self._flush()
+        return RangeCoder(self._state.lower_bound, self._state.range)
+
+    def finish(self):  # encoder.rs:40-46
+        if self._finished:
+            raise FinishedError("finish twice")
+        self._flush(finish=True)
+        self._finished = True
+        return bytes(self._code)
+
+    def _count(self, i):
+        if i >= self._staged0:
+            self._flush()
+        if i >= len(self._counts):
+            raise RangeCoderError(f"symbol {i} was not coded (an earlier symbol failed)")
+        return self._counts[i]
+
+    def _flush(self, finish=False):
+        n = len(self._trip) // 3
+        if n == 0 and not finish:
+            return
+        if self._state.flags:
+            _raise_for_flag(self._state.flags, "encode")
+        ctx = self._ctx or default_context()
+        trip = np.array(self._trip, dtype=np.uint32)
+        cap = N.stream_max_bytes(n, finish)
+        out = np.empty(max(cap, 1), np.uint8)
+        nb = np.empty(max(n, 1), np.uint8)
+        out_len = ctypes.c_uint64()
+        fl = ctypes.c_uint32()
+        n0 = self._state.n
+        rc = ctx._lib.rc_stream_encode_host(ctx.handle, ctypes.byref(self._state), _np_ptr(trip),
+                                            n, _np_ptr(out), cap, ctypes.byref(out_len),
+                                            _np_ptr(nb), 1 if finish else 0, ctypes.byref(fl))
+        if rc not in (N.RC_OK, N.RC_E_CHUNK):
+            N.check(rc, "rc_stream_encode_host")
+        self._code += out[: out_len.value].tobytes()
+        self._counts += nb[: self._state.n - n0].tobytes()
+        self._staged0 += n
+        self._trip = []
+        if fl.value:
+            _raise_for_flag(fl.value, f"encode (symbol {self._state.n})")
 
 
 class Decoder:
-    """Decoder (src/decoder.rs:6-55) for ONE stream; n_symbols is the out-of-band count the
-    reference's caller also supplies (sample_impl.rs:113-120)."""
+    """Decoder (src/decoder.rs:6-55) for ONE stream, with the reference's per-call semantics.
 
-    def __init__(self, code, n_symbols=None):
-        self._code = bytes(code)
-        if len(self._code) < 8:  # Decoder::new panics (decoder.rs:21,33)
+    Decoder(code) runs Decoder::new (the first 8 bytes; a shorter code raises as the reference
+    panics).  decode(pmodel) reads the model's table at that call (c_freq / cum_freq /
+    total_freq over alphabet_count()) and decodes with FreqTable::find_index's binary search
+    and param_update (sample_impl.rs:27-45, decoder.rs:38-54), evaluated on the GPU by the
+    resumable stream kernel.  Symbols are decoded ahead in blocks that double while the table
+    stays the same; when the caller's table changes (an adaptive PModel), the state at that
+    symbol is re-derived and decoding continues under the new table, so every symbol is decoded
+    with the table the caller held at its call.  The user's find_index is not called: for a
+    PModel whose (c, cum) intervals tile [0, total) — the contract decoding relies on — it
+    returns what the binary search returns.  n_symbols (optional, out-of-band as in
+    sample_impl.rs:113-120) only bounds the decode-ahead."""
+
+    MAX_BLOCK = 1 << 20
+
+    def __init__(self, code, n_symbols=None, ctx=None):
+        self._ctx = ctx or default_context()
+        self._code = np.frombuffer(bytes(code), dtype=np.uint8)
+        self._limit = None if n_symbols is None else int(n_symbols)
+        self._arrays = (None, None)  # table signature -> (c, cum) uint32 arrays
+        st = N.StreamState.fresh()
+        if len(self._code) < 8:  # Decoder::new panics (decoder.rs:21, :33)
             raise TruncatedStreamError("code shorter than 8 bytes")
-        self._n = n_symbols
-        self._out = None
-        self._pos = 0
+        self._run(st, ((1,), (0,), 1), 0)  # Decoder::new: prime the data window
+        self._start = st            # state at the first symbol of the current block
+        self._end = st              # state after the block (before a failing symbol)
+        self._buf = np.zeros(0, np.uint8)
+        self._bpos = 0
+        self._sig = None
+        self._err = 0               # flag of the symbol after the block, if it failed
+        self._block = 1
+        self._taken = 0             # symbols returned
 
-    def decode(self, pmodel):
-        if self._out is None:
-            if self._n is None:
-                raise RangeCoderError("Decoder(code, n_symbols): the symbol count is out-of-band")
-            m = _snapshot(pmodel)
-            self._out = decode_chunks(m, [self._code], [self._n])[0]
-        if self._pos >= len(self._out):
-            raise RangeCoderError("more decode() calls than n_symbols")
-        s = int(self._out[self._pos])
-        self._pos += 1
-        return s
+    @classmethod
+    def new(cls, code):  # decoder.rs:14-23
+        return cls(code)
+
+    def _run(self, st, sig, n):
+        """Decode n symbols from state st (updated) under table sig; returns (symbols, flags)."""
+        if self._arrays[0] != sig:
+            self._arrays = (sig, (np.array(sig[0], np.uint32), np.array(sig[1], np.uint32)))
+        c, cum = self._arrays[1]
+        if not 1 <= len(c) <= 256 or len(cum) != len(c):
+            raise RangeCoderError(f"alphabet of {len(c)} symbols (the GPU decoders take 1..256)")
+        out = np.empty(max(n, 1), np.uint8)
+        fl = ctypes.c_uint32()
+        n0 = st.n
+        ctx = self._ctx
+        rc = ctx._lib.rc_stream_decode_host(ctx.handle, _np_ptr(c), _np_ptr(cum), len(c),
+                                            _u32(sig[2], "total_freq"), ctypes.byref(st),
+                                            _np_ptr(self._code), len(self._code), _np_ptr(out),
+                                            n, ctypes.byref(fl))
+        if rc not in (N.RC_OK, N.RC_E_CHUNK):
+            N.check(rc, "rc_stream_decode_host")
+        return out[: st.n - n0], fl.value
+
+    @staticmethod
+    def _copy(st):
+        return N.StreamState.from_buffer_copy(st)
+
+    def _here(self):
+        """The state at the current symbol (re-derived inside a block; the block then starts
+        here, so the next call needs no re-derivation)."""
+        if self._bpos == 0:
+            return self._start
+        if self._bpos == len(self._buf):
+            st = self._copy(self._end)
+            st.flags = 0
+            return st
+        st = self._copy(self._start)
+        self._run(st, self._sig, self._bpos)
+        self._start, self._buf, self._bpos = st, self._buf[self._bpos:], 0
+        return st
+
+    def decode(self, pmodel):  # decoder.rs:38-54
+        sig = _table_of(pmodel)
+        if sig == self._sig and self._bpos < len(self._buf):
+            s = self._buf[self._bpos]
+            self._bpos += 1
+            self._taken += 1
+            return int(s)
+        if sig == self._sig and self._err:  # the reference panics / hangs at this symbol
+            _raise_for_flag(self._err, f"decode (symbol {self._taken})")
+        if sig == self._sig and self._bpos == len(self._buf):
+            self._block = min(2 * self._block, self.MAX_BLOCK)
+        else:
+            self._block = 1
+        st = self._copy(self._here())
+        n = self._block
+        if self._limit is not None:
+            n = max(1, min(n, self._limit - self._taken))
+        start = self._copy(st)
+        syms, fl = self._run(st, sig, n)
+        self._start, self._end, self._buf, self._bpos = start, st, syms, 0
+        self._sig, self._err = sig, fl
+        if len(syms) == 0:
+            _raise_for_flag(fl, f"decode (symbol {self._taken})")
+        self._bpos = 1
+        self._taken += 1
+        return int(syms[0])
+
+    def range_coder(self):  # decoder.rs:24-26 (a snapshot)
+        st = self._here()
+        return RangeCoder(st.lower_bound, st.range)
+
+    def data(self):  # decoder.rs:27-29
+        return int(self._here().data)
 
 
-_snap_cache = {}
+def stream_states(n, device=None):
+    """n fresh rc_stream_state on the device (RC_STREAM_STATE_INIT), as an int64 tensor of shape
+    (n, 6): lower_bound, range, data, pos, n, flags | stage << 32."""
+    torch = _torch()
+    st = torch.zeros((n, 6), dtype=torch.int64, device=device or "cuda")
+    st[:, 1] = -1  # range = u64::MAX
+    return st
 
 
-def _snapshot(pmodel):
-    if isinstance(pmodel, StaticModel):
-        return pmodel
-    key = id(pmodel)
-    n = pmodel.alphabet_count()
-    sig = (tuple(pmodel.c_freq(i) for i in range(n)), tuple(pmodel.cum_freq(i) for i in range(n)),
-           pmodel.total_freq())
-    hit = _snap_cache.get(key)
-    if hit is not None and hit[0] == sig:
-        return hit[1]
-    m = StaticModel(sig[0], sig[1], sig[2])
-    _snap_cache[key] = (sig, m)
-    return m
+def stream_encode_batch(ctx, states, triples, sym_off, out, out_off, out_len=None, nbytes=None,
+                        finish=False, flags=None):
+    """rc_stream_encode on torch tensors (async on torch's current stream): n = states.shape[0]
+    streams, triples uint32/int32 (3 per symbol), sym_off int64[n+1] indexing the triples, out
+    uint8 with slots out_off int64[n+1].  Returns (out_len, flags)."""
+    torch = _torch()
+    n = states.shape[0]
+    _check_dev(states, "states", (torch.int64,))
+    _check_dev(triples, "triples", (torch.int32, torch.uint32))
+    _check_dev(out, "out", (torch.uint8,))
+    for name, t in (("sym_off", sym_off), ("out_off", out_off)):
+        _check_dev(t, name, (torch.int64, torch.uint64))
+        if t.numel() != n + 1:
+            raise ValueError(f"{name} must have n_streams + 1 entries")
+    if nbytes is not None:
+        _check_dev(nbytes, "nbytes", (torch.uint8,))
+    if out_len is None:
+        out_len = torch.empty(max(n, 1), dtype=torch.int64, device=states.device)
+    if flags is None:
+        flags = torch.empty(max(n, 1), dtype=torch.int32, device=states.device)
+    ctx.bind_stream()
+    N.check(ctx._lib.rc_stream_encode(ctx.handle, _ptr(states), _ptr(triples), _ptr(sym_off), n,
+                                      _ptr(out), _ptr(out_off), _ptr(out_len), _ptr(nbytes),
+                                      1 if finish else 0, _ptr(flags)), "rc_stream_encode")
+    return out_len[:n], flags[:n]
+
+
+def stream_decode_batch(ctx, c, cum, total, states, code, code_off, code_len, syms, sym_off,
+                        flags=None):
+    """rc_stream_decode on torch tensors: one (c, cum, total) table (uint32/int32 device
+    tensors) for every stream's next sym_off[k+1] - sym_off[k] symbols.  Returns flags."""
+    torch = _torch()
+    n = states.shape[0]
+    _check_dev(states, "states", (torch.int64,))
+    for name, t in (("c", c), ("cum", cum)):
+        _check_dev(t, name, (torch.int32, torch.uint32))
+    _check_dev(code, "code", (torch.uint8,))
+    _check_dev(syms, "syms", (torch.uint8,))
+    for name, t in (("code_off", code_off), ("code_len", code_len), ("sym_off", sym_off)):
+        _check_dev(t, name, (torch.int64, torch.uint64))
+    if flags is None:
+        flags = torch.empty(max(n, 1), dtype=torch.int32, device=states.device)
+    ctx.bind_stream()
+    rc = ctx._lib.rc_stream_decode(ctx.handle, _ptr(c), _ptr(cum), c.numel(),
+                                   ctypes.c_uint32(int(total) & 0xFFFFFFFF), _ptr(states),
+                                   _ptr(code), _ptr(code_off), _ptr(code_len), _ptr(syms),
+                                   _ptr(sym_off), n, _ptr(flags))
+    N.check(rc, "rc_stream_decode")
+    return flags[:n]
 
 
 # ----------------------------------------------------------------------------- host streaming

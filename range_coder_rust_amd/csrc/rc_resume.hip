@@ -1,0 +1,402 @@
+// rc_resume.hip — resumable streams: the reference's per-call Encoder::encode / Decoder::decode
+// with the model read on every call (include/range_coder.h, rc_stream_*).
+//
+// The batch kernels (rc_encode.hip, rc_decode.inc) code whole chunks against one table held in
+// LDS.  The reference's public surface is per call instead: Encoder::encode reads the caller's
+// (c_freq(i), cum_freq(i), total_freq()) at that moment (encoder.rs:24-31) and Decoder::decode
+// runs find_index and reads the table again (decoder.rs:38-50), so a caller may change its
+// PModel between calls.  These kernels keep one stream's state (RangeCoder, decoder data window,
+// 64-bit stream position) in rc_stream_state between launches, and take per-symbol triples
+// (encode) or the table of the next n symbols (decode).  One lane per stream: the host mirrors
+// (api.py Encoder / Decoder, range_coder.hpp) run one stream, so this path is latency-, not
+// bandwidth-bound; the arithmetic is the reference's, branch for branch, with its panics and
+// endless loops turned into sticky flags:
+//   total == 0                       -> RC_F_BAD_MODEL (u64 / 0, range_coder.rs:38-40)
+//   low + r*cum overflows            -> RC_F_BAD_MODEL (LowerBoundOverflow, :68-81)
+//   range == r*c == 0                -> RC_F_ZERO_FREQ / RC_F_CORRUPT (:83-85 never ends)
+//   low + range overflows            -> RC_F_BAD_MODEL (upper_bound().unwrap(), :138-146)
+//   decoder needs a byte past the end -> RC_F_TRUNCATED (pop_front().unwrap(), decoder.rs:33)
+// u64 products wrap (release-build semantics of the reference).
+#include "rc_common.h"
+
+#include <string.h>
+
+#include <algorithm>
+
+#define RWG 64
+#define TOP8 (1ull << 56)  // range_coder.rs:23
+
+static_assert(sizeof(rc_stream_state) == 48, "rc_stream_state layout");
+
+namespace {
+
+// RangeCoder::param_update up to the renormalisation loops: the narrowed interval, or a flag
+struct Narrow {
+  u64 low, range;
+  u32 err;
+};
+
+static __device__ __forceinline__ Narrow narrow(u64 low, u64 range, u32 c, u32 cum, u32 total,
+                                                u32 zero_flag) {
+  Narrow o{low, range, 0u};
+  if (total == 0) {  // range_par_total (range_coder.rs:38-40) divides by zero
+    o.err = RC_F_BAD_MODEL;
+    return o;
+  }
+  const u64 r = range / (u64)total;
+  const u64 nr = r * (u64)c;     // range_coder.rs:65
+  const u64 add = r * (u64)cum;  // :68
+  const u64 nl = low + add;
+  if (nl < add) o.err = RC_F_BAD_MODEL;          // overflowing_add -> Err (:68-81)
+  else if (nr == 0) o.err = zero_flag;           // no_carry_expansion never terminates
+  else if (nl + nr < nr) o.err = RC_F_BAD_MODEL;  // upper_bound() overflow (:138-146)
+  o.low = nl;
+  o.range = nr;
+  return o;
+}
+
+// bytes the two renormalisation loops settle from (low, range), without applying them
+static __device__ __forceinline__ u32 settle_count(u64 low, u64 range) {
+  u32 k = 0;
+  while (((low ^ (low + range)) >> 56) == 0) {  // no_carry_expansion (:110-116)
+    low <<= 8;
+    range <<= 8;
+    ++k;
+  }
+  while (range < TOP16) {  // range_reduction_expansion (:126-135)
+    range = ~low & (TOP16 - 1);
+    low <<= 8;
+    range <<= 8;
+    ++k;
+  }
+  return k;
+}
+
+__global__ __launch_bounds__(RWG) void k_stream_encode(
+    rc_stream_state* __restrict__ st, const u32* __restrict__ trip, const u64* __restrict__ sym_off,
+    u32 n_streams, uint8_t* __restrict__ out, const u64* __restrict__ out_off,
+    u64* __restrict__ out_len, uint8_t* __restrict__ nbytes, u32 finish,
+    u32* __restrict__ flags) {
+  const u32 k = blockIdx.x * RWG + threadIdx.x;
+  if (k >= n_streams) return;
+  RC_VGPR_FLOOR_48();
+  rc_stream_state S = st[k];
+  const u64 s0 = sym_off[k], n = sym_off[k + 1] - s0;
+  uint8_t* o = out + out_off[k];
+  const u64 cap = out_off[k + 1] - out_off[k];
+  out_len[k] = 0;
+  if (S.flags) {  // the reference panicked (or hung) at an earlier call
+    flags[k] = S.flags;
+    return;
+  }
+  if (S.stage == 2) {  // Encoder::finish took the encoder by value (encoder.rs:40)
+    S.flags = RC_F_FINISHED;
+    st[k] = S;
+    flags[k] = S.flags;
+    return;
+  }
+  if (cap < RC_STREAM_MAX_BYTES(n, finish)) {  // not sticky: the caller retries, nothing changed
+    flags[k] = RC_F_CAPACITY;
+    return;
+  }
+  u64 low = S.lower_bound, range = S.range, w = 0;
+  for (u64 i = 0; i < n; ++i) {  // Encoder::encode (encoder.rs:24-37)
+    const u32* t = trip + 3 * (s0 + i);
+    const Narrow q = narrow(low, range, t[0], t[1], t[2], RC_F_ZERO_FREQ);
+    if (q.err) {
+      S.flags = q.err;
+      break;
+    }
+    low = q.low;
+    range = q.range;
+    u32 nb = 0;
+    while (((low ^ (low + range)) >> 56) == 0) {  // no_carry_expansion (:110-116)
+      gstore8(o + w++, (u32)(low >> 56));       // left_shift (:95-100)
+      low <<= 8;
+      range <<= 8;
+      ++nb;
+    }
+    while (range < TOP16) {  // range_reduction_expansion (:126-135)
+      range = ~low & (TOP16 - 1);
+      gstore8(o + w++, (u32)(low >> 56));
+      low <<= 8;
+      range <<= 8;
+      ++nb;
+    }
+    if (nbytes) gstore8(nbytes + s0 + i, nb);  // encode()'s return value (encoder.rs:34-36)
+    S.n += 1;
+  }
+  if (finish && !S.flags) {  // Encoder::finish: 8 x left_shift (encoder.rs:40-46)
+    for (int j = 0; j < 8; ++j) {
+      gstore8(o + w++, (u32)(low >> 56));
+      low <<= 8;
+      range <<= 8;
+    }
+    S.stage = 2;
+  } else if (S.stage == 0) {
+    S.stage = 1;
+  }
+  S.lower_bound = low;
+  S.range = range;
+  S.pos += w;
+  st[k] = S;
+  out_len[k] = w;
+  flags[k] = S.flags;
+}
+
+__global__ __launch_bounds__(RWG) void k_stream_decode(
+    const u32* __restrict__ c_tab, const u32* __restrict__ cum_tab, u32 n_alpha, u32 total,
+    rc_stream_state* __restrict__ st, const uint8_t* __restrict__ code,
+    const u64* __restrict__ code_off, const u64* __restrict__ code_len,
+    uint8_t* __restrict__ syms, const u64* __restrict__ sym_off, u32 n_streams,
+    u32* __restrict__ flags) {
+  __shared__ u32 s_c[256], s_cum[256];
+  for (u32 j = threadIdx.x; j < n_alpha; j += RWG) {
+    s_c[j] = c_tab[j];
+    s_cum[j] = cum_tab[j];
+  }
+  __syncthreads();
+  const u32 k = blockIdx.x * RWG + threadIdx.x;
+  if (k >= n_streams) return;
+  RC_VGPR_FLOOR_64();
+  rc_stream_state S = st[k];
+  const uint8_t* cp = code + code_off[k];
+  const u64 clen = code_len[k];
+  const u64 s0 = sym_off[k], n = sym_off[k + 1] - s0;
+  if (S.flags) {
+    flags[k] = S.flags;
+    return;
+  }
+  if (S.stage == 0) {  // Decoder::new: the first 8 bytes (decoder.rs:14-23)
+    if (clen < 8) {
+      S.flags = RC_F_TRUNCATED;
+      st[k] = S;
+      flags[k] = S.flags;
+      return;
+    }
+    u64 d = 0;
+    for (int j = 0; j < 8; ++j) d = (d << 8) | cp[j];
+    S.data = d;
+    S.pos = 8;
+    S.stage = 1;
+  }
+  u64 low = S.lower_bound, range = S.range, data = S.data, pos = S.pos;
+  for (u64 i = 0; i < n; ++i) {  // Decoder::decode (decoder.rs:38-54)
+    if (total == 0) {            // find_index's range_par_total divides by zero
+      S.flags = RC_F_BAD_MODEL;
+      break;
+    }
+    // FreqTable::find_index (sample_impl.rs:27-45): rfreq, then the binary search over cum
+    const u64 rfreq = (data - low) / (range / (u64)total);
+    u32 left = 0, right = n_alpha - 1;
+    while (left < right) {
+      const u32 mid = (left + right) >> 1;
+      if ((u64)s_cum[mid + 1] <= rfreq) left = mid + 1;
+      else right = mid;
+    }
+    const Narrow q = narrow(low, range, s_c[left], s_cum[left], total, RC_F_CORRUPT);
+    if (q.err) {
+      S.flags = q.err;
+      break;
+    }
+    const u32 nb = settle_count(q.low, q.range);
+    if (pos + nb > clen) {  // shift_left_buffer pops past the end (decoder.rs:31-35)
+      S.flags = RC_F_TRUNCATED;
+      break;
+    }
+    low = q.low;
+    range = q.range;
+    while (((low ^ (low + range)) >> 56) == 0) {
+      low <<= 8;
+      range <<= 8;
+    }
+    while (range < TOP16) {
+      range = ~low & (TOP16 - 1);
+      low <<= 8;
+      range <<= 8;
+    }
+    for (u32 j = 0; j < nb; ++j) data = (data << 8) | cp[pos++];
+    gstore8(syms + s0 + i, left);
+    S.n += 1;
+  }
+  S.lower_bound = low;
+  S.range = range;
+  S.data = data;
+  S.pos = pos;
+  st[k] = S;
+  flags[k] = S.flags;
+}
+
+struct Dev {
+  int prev = -1;
+  explicit Dev(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~Dev() {
+    int now = -1;
+    if (prev >= 0 && hipGetDevice(&now) == hipSuccess && now != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// stream-ordered device scratch for the host variants, freed on every return path
+struct Scratch {
+  hipStream_t s;
+  void* p = nullptr;
+  Scratch(hipStream_t s_, size_t n) : s(s_) {
+    if (hipMallocAsync(&p, std::max<size_t>(n, 16), s) != hipSuccess) p = nullptr;
+  }
+  ~Scratch() {
+    if (p) {
+      (void)hipFreeAsync(p, s);
+      (void)hipStreamSynchronize(s);
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+rc_status rc_ctx_stream_(rc_ctx* ctx, hipStream_t* s, int* device);  // rc_kernels.hip
+
+rc_status rc_stream_encode(rc_ctx* ctx, rc_stream_state* states, const uint32_t* triples,
+                           const uint64_t* sym_off, uint32_t n_streams, uint8_t* out,
+                           const uint64_t* out_off, uint64_t* out_len, uint8_t* nbytes,
+                           uint32_t finish, uint32_t* flags) {
+  hipStream_t s;
+  int dev;
+  if (rc_ctx_stream_(ctx, &s, &dev) != RC_OK || n_streams > RC_MAX_CHUNKS) return RC_E_ARG;
+  if (n_streams == 0) return RC_OK;
+  if (!states || !triples || !sym_off || !out || !out_off || !out_len || !flags) return RC_E_ARG;
+  Dev g(dev);
+  hipLaunchKernelGGL(k_stream_encode, dim3((n_streams + RWG - 1) / RWG), dim3(RWG), 0, s,
+                     states, triples, sym_off, n_streams, out, out_off, out_len, nbytes, finish,
+                     flags);
+  return hipGetLastError() == hipSuccess ? RC_OK : RC_E_DEVICE;
+}
+
+rc_status rc_stream_decode(rc_ctx* ctx, const uint32_t* c, const uint32_t* cum,
+                           uint32_t n_symbols, uint32_t total_freq, rc_stream_state* states,
+                           const uint8_t* code, const uint64_t* code_off,
+                           const uint64_t* code_len, uint8_t* syms, const uint64_t* sym_off,
+                           uint32_t n_streams, uint32_t* flags) {
+  hipStream_t s;
+  int dev;
+  if (rc_ctx_stream_(ctx, &s, &dev) != RC_OK || n_streams > RC_MAX_CHUNKS) return RC_E_ARG;
+  if (n_symbols < 1 || n_symbols > 256) return RC_E_BAD_MODEL;
+  if (n_streams == 0) return RC_OK;
+  if (!c || !cum || !states || !code || !code_off || !code_len || !syms || !sym_off || !flags)
+    return RC_E_ARG;
+  Dev g(dev);
+  hipLaunchKernelGGL(k_stream_decode, dim3((n_streams + RWG - 1) / RWG), dim3(RWG), 0, s, c,
+                     cum, n_symbols, total_freq, states, code, code_off, code_len, syms, sym_off,
+                     n_streams, flags);
+  return hipGetLastError() == hipSuccess ? RC_OK : RC_E_DEVICE;
+}
+
+rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint32_t* triples,
+                                uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
+                                uint8_t* nbytes, uint32_t finish, uint32_t* flags_out) {
+  hipStream_t s;
+  int dev;
+  if (rc_ctx_stream_(ctx, &s, &dev) != RC_OK || !state || !out_len || (n && !triples))
+    return RC_E_ARG;
+  const u64 need = RC_STREAM_MAX_BYTES(n, finish);
+  *out_len = 0;
+  if (out_cap < need || (need && !out)) {
+    if (flags_out) *flags_out = RC_F_CAPACITY;
+    return RC_E_CAPACITY;
+  }
+  Dev g(dev);
+  // layout: state | offsets (4 x u64) | out_len | flags | triples | nbytes | out
+  const size_t o_off = 64, o_len = o_off + 32, o_fl = o_len + 16, o_tr = o_fl + 16;
+  const size_t o_nb = o_tr + ((12 * n + 15) & ~15ull), o_out = o_nb + ((n + 15) & ~15ull);
+  Scratch sc(s, o_out + need);
+  if (!sc.p) return RC_E_DEVICE;
+  char* d = (char*)sc.p;
+  const u64 offs[4] = {0, n, 0, need};  // sym_off[0..1], out_off[0..1]
+  bool ok = hipMemcpyAsync(d, state, sizeof *state, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemcpyAsync(d + o_off, offs, sizeof offs, hipMemcpyHostToDevice, s) == hipSuccess &&
+            (!n || hipMemcpyAsync(d + o_tr, triples, 12 * n, hipMemcpyHostToDevice, s) ==
+                       hipSuccess);
+  if (!ok) return RC_E_DEVICE;
+  hipLaunchKernelGGL(k_stream_encode, dim3(1), dim3(RWG), 0, s, (rc_stream_state*)d,
+                     (const u32*)(d + o_tr), (const u64*)(d + o_off), 1u, (uint8_t*)(d + o_out),
+                     (const u64*)(d + o_off + 16), (u64*)(d + o_len),
+                     nbytes ? (uint8_t*)(d + o_nb) : (uint8_t*)nullptr, finish,
+                     (u32*)(d + o_fl));
+  if (hipGetLastError() != hipSuccess) return RC_E_DEVICE;
+  rc_stream_state nst;
+  u32 fl = 0;
+  ok = hipMemcpyAsync(&nst, d, sizeof nst, hipMemcpyDeviceToHost, s) == hipSuccess &&
+       hipMemcpyAsync(&fl, d + o_fl, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+       hipStreamSynchronize(s) == hipSuccess;
+  if (!ok) return RC_E_DEVICE;
+  const u64 w = nst.pos - state->pos;
+  if (w && hipMemcpyAsync(out, d + o_out, w, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return RC_E_DEVICE;
+  if (nbytes && n && hipMemcpyAsync(nbytes, d + o_nb, n, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return RC_E_DEVICE;
+  if (hipStreamSynchronize(s) != hipSuccess) return RC_E_DEVICE;
+  *state = nst;
+  *out_len = w;
+  if (flags_out) *flags_out = fl;
+  return fl ? RC_E_CHUNK : RC_OK;
+}
+
+rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* cum,
+                                uint32_t n_symbols, uint32_t total_freq, rc_stream_state* state,
+                                const uint8_t* code, uint64_t code_len, uint8_t* syms,
+                                uint64_t n, uint32_t* flags_out) {
+  hipStream_t s;
+  int dev;
+  if (rc_ctx_stream_(ctx, &s, &dev) != RC_OK || !state || !c || !cum || (n && !syms) ||
+      (code_len && !code))
+    return RC_E_ARG;
+  if (n_symbols < 1 || n_symbols > 256) return RC_E_BAD_MODEL;
+  // the window this call can read: Decoder::new's 8 bytes and <= 12 per symbol
+  const u64 p0 = state->stage == 0 ? 0 : state->pos;
+  if (p0 > code_len) return RC_E_ARG;
+  const u64 wlen = std::min<u64>(code_len - p0, (state->stage == 0 ? 8 : 0) + 12 * n);
+  Dev g(dev);
+  // layout: state | offsets: code_off, code_len, sym_off[0..1] | flags | c | cum | window | syms
+  const size_t o_off = 64, o_fl = o_off + 32, o_c = o_fl + 16, o_cum = o_c + 1024;
+  const size_t o_win = o_cum + 1024, o_sym = o_win + ((wlen + 15) & ~15ull);
+  Scratch sc(s, o_sym + n);
+  if (!sc.p) return RC_E_DEVICE;
+  char* d = (char*)sc.p;
+  rc_stream_state rel = *state;
+  rel.pos -= p0;  // the window starts at p0 (stage 0: at the stream start, pos is unused)
+  const u64 offs[4] = {0, wlen, 0, n};
+  bool ok = hipMemcpyAsync(d, &rel, sizeof rel, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemcpyAsync(d + o_off, offs, sizeof offs, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemcpyAsync(d + o_c, c, 4ull * n_symbols, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemcpyAsync(d + o_cum, cum, 4ull * n_symbols, hipMemcpyHostToDevice, s) ==
+                hipSuccess &&
+            (!wlen || hipMemcpyAsync(d + o_win, code + p0, wlen, hipMemcpyHostToDevice, s) ==
+                          hipSuccess);
+  if (!ok) return RC_E_DEVICE;
+  hipLaunchKernelGGL(k_stream_decode, dim3(1), dim3(RWG), 0, s, (const u32*)(d + o_c),
+                     (const u32*)(d + o_cum), n_symbols, total_freq, (rc_stream_state*)d,
+                     (const uint8_t*)(d + o_win), (const u64*)(d + o_off),
+                     (const u64*)(d + o_off + 8), (uint8_t*)(d + o_sym),
+                     (const u64*)(d + o_off + 16), 1u, (u32*)(d + o_fl));
+  if (hipGetLastError() != hipSuccess) return RC_E_DEVICE;
+  rc_stream_state nst;
+  u32 fl = 0;
+  ok = hipMemcpyAsync(&nst, d, sizeof nst, hipMemcpyDeviceToHost, s) == hipSuccess &&
+       hipMemcpyAsync(&fl, d + o_fl, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+       hipStreamSynchronize(s) == hipSuccess;
+  if (!ok) return RC_E_DEVICE;
+  const u64 got = nst.n - state->n;
+  if (got && hipMemcpyAsync(syms, d + o_sym, got, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return RC_E_DEVICE;
+  if (hipStreamSynchronize(s) != hipSuccess) return RC_E_DEVICE;
+  nst.pos += p0;
+  *state = nst;
+  if (flags_out) *flags_out = fl;
+  return fl ? RC_E_CHUNK : RC_OK;
+}
+
+}  // extern "C"

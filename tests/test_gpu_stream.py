@@ -1,0 +1,305 @@
+"""The reference's per-call surface on the GPU (rc_stream_* kernels, rc_resume.hip) against the
+oracles: Encoder / Decoder with a PModel the caller changes between calls, encode()'s byte
+counts, peek_code, range_coder / data, Decoder without a symbol count, errors at the exact
+call; and the batch device entry points against orc_stream_* with random (even inconsistent)
+tables, garbage streams, split calls and 64-bit stream positions."""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import range_coder_rust_amd as rc  # noqa: E402
+from oracle import cpu, ref_literal as R  # noqa: E402
+from gpu_helpers import dev  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return rc.default_context(0)
+
+
+SAMPLE = [2, 1, 1, 4, 1, 4, 2, 1, 0, 1, 5, 9, 8, 7, 6, 5]
+
+
+def _sample_table():
+    sd = rc.FreqTable(10)
+    for i in SAMPLE:
+        sd.add_alphabet_freq(i)
+    sd.calc_cum()
+    return sd
+
+
+def test_sample_impl_reference_surface(ctx):
+    """examples/sample_impl.rs:72-128 verbatim: Decoder::new(code) takes no count."""
+    sd = _sample_table()
+    encoder = rc.Encoder.new()
+    rets = [encoder.encode(sd, i) for i in SAMPLE]
+    code = encoder.finish()
+    assert code.hex() == "64475f8970365a2f83b20246c0"
+    ref = R.Encoder()
+    rt = R.FreqTable.from_counts(sd.c)
+    assert [int(r) for r in rets] == [ref.encode(rt, i) for i in SAMPLE]
+    decoder = rc.Decoder.new(code)
+    assert [decoder.decode(sd) for _ in SAMPLE] == SAMPLE
+
+
+class AdaptiveFreqTable(rc.FreqTable):
+    """A caller-side adaptive model: the mirror FreqTable, updated after every symbol with the
+    rule of oracle/ref_literal.py AdaptiveModel (what a reference user would write on top of
+    the PModel trait)."""
+
+    def __init__(self, n, inc, limit, period):
+        super().__init__(n)
+        self.c = [1] * n
+        self.calc_cum()
+        self.inc, self.limit, self.period = inc, limit, period
+
+    def update(self, s, i):
+        self.c[s] += self.inc
+        if (i + 1) % self.period == 0 and sum(self.c) > self.limit:
+            self.c = [(x + 1) >> 1 for x in self.c]
+        self.calc_cum()
+
+
+def _zipfish(n, seed, alpha=256):
+    rng = random.Random(seed)
+    return [min(alpha - 1, int(rng.paretovariate(1.15))) for _ in range(n)]
+
+
+def test_model_mutated_between_encode_calls(ctx):
+    syms = _zipfish(5000, 1)
+    want = R.encode_adaptive_stream(256, 32, 4000, 64, syms)
+    m = AdaptiveFreqTable(256, 32, 4000, 64)
+    ref_m = R.AdaptiveModel(256, 32, 4000, 64)
+    ref = R.Encoder()
+    enc = rc.Encoder()
+    rets, ref_rets = [], []
+    for i, s in enumerate(syms):
+        rets.append(enc.encode(m, s))
+        ref_rets.append(ref.encode(ref_m, s))
+        m.update(s, i)
+        ref_m.update(s, i)
+        if i in (0, 7, 100, 2047, 4000):  # peek_code / range_coder mid-stream
+            assert enc.peek_code() == bytes(ref.code)
+            assert enc.range_coder == rc.RangeCoder(ref.range_coder.lower_bound,
+                                                    ref.range_coder.range)
+    code = enc.finish()
+    assert code == want
+    assert [int(r) for r in rets] == ref_rets
+    with pytest.raises(rc.FinishedError):
+        enc.encode(m, 0)
+
+
+def test_model_mutated_between_decode_calls(ctx):
+    syms = _zipfish(4000, 2)
+    code = R.encode_adaptive_stream(256, 32, 4000, 64, syms)
+    m = AdaptiveFreqTable(256, 32, 4000, 64)
+    ref = R.Decoder(code)
+    ref_m = R.AdaptiveModel(256, 32, 4000, 64)
+    dec = rc.Decoder(code)
+    out = []
+    for i in range(len(syms)):
+        s = dec.decode(m)
+        assert s == ref.decode(ref_m)
+        out.append(s)
+        m.update(s, i)
+        ref_m.update(s, i)
+        if i in (0, 9, 1000, 3999):
+            assert dec.data() == ref.data
+            assert dec.range_coder() == rc.RangeCoder(ref.range_coder.lower_bound,
+                                                      ref.range_coder.range)
+    assert out == syms
+
+
+def test_static_then_switch_models_mid_stream(ctx):
+    """Decode-ahead blocks under one table, then a different table from symbol 3000 on."""
+    a = rc.FreqTable.from_counts([1 + (i * 7) % 13 for i in range(256)])
+    b = rc.FreqTable.from_counts([1 + (i * 3) % 29 for i in range(256)])
+    rng = random.Random(3)
+    syms = [rng.randrange(256) for _ in range(6000)]
+    enc = rc.Encoder()
+    for i, s in enumerate(syms):
+        enc.encode(a if i < 3000 else b, s)
+    code = enc.finish()
+    ref = R.Encoder()
+    ra, rb = R.FreqTable.from_counts(a.c), R.FreqTable.from_counts(b.c)
+    for i, s in enumerate(syms):
+        ref.encode(ra if i < 3000 else rb, s)
+    assert code == bytes(ref.finish())
+    dec = rc.Decoder(code)
+    got = [dec.decode(a) for _ in range(2500)]
+    st = dec.range_coder()  # re-derived inside a decode-ahead block
+    got += [dec.decode(a) for _ in range(500)]
+    got += [dec.decode(b) for _ in range(3000)]
+    assert got == syms
+    rdec = R.Decoder(code)
+    for _ in range(2500):
+        rdec.decode(ra)
+    assert st == rc.RangeCoder(rdec.range_coder.lower_bound, rdec.range_coder.range)
+
+
+def test_errors_at_the_reference_call(ctx):
+    sd = _sample_table()
+    enc = rc.Encoder()
+    with pytest.raises(rc.ZeroFrequencyError):
+        enc.encode(sd, 3)  # c_freq(3) == 0: the reference never terminates
+    with pytest.raises(rc.BadSymbolError):
+        enc.encode(sd, 10)  # sample_impl.rs:19 unwrap
+    code = rc.Encoder()
+    for i in SAMPLE:
+        code.encode(sd, i)
+    code = code.finish()
+    # decoding past the end: the reference panics in shift_left_buffer at some call k
+    ref = R.Decoder(code)
+    rt = R.FreqTable.from_counts(sd.c)
+    k = 0
+    while True:
+        try:
+            ref.decode(rt)
+        except R.ReferencePanic:
+            break
+        k += 1
+    dec = rc.Decoder(code)
+    for _ in range(k):
+        dec.decode(sd)
+    with pytest.raises(rc.TruncatedStreamError):
+        dec.decode(sd)
+    with pytest.raises(rc.TruncatedStreamError):
+        rc.Decoder(code[:7])
+
+
+def _random_triples(rng, n):
+    t = []
+    for _ in range(n):
+        total = rng.choice([256, 65536, rng.randint(1, 2 ** 32 - 1)])
+        c = rng.randint(1, total) if rng.random() < 0.97 else rng.randint(0, 2 ** 32 - 1)
+        cum = rng.randint(0, total - min(c, total)) if rng.random() < 0.97 else \
+            rng.randint(0, 2 ** 32 - 1)
+        t.append((c, cum, total if rng.random() < 0.995 else 0))
+    return t
+
+
+def test_batch_stream_encode_split_calls_vs_oracle(ctx):
+    rng = random.Random(5)
+    ns = 150
+    streams = [_random_triples(rng, rng.randint(0, 300)) for _ in range(ns)]
+    # oracle: one call each
+    want = []
+    for t in streams:
+        st = cpu.Stream.fresh()
+        f, b, nb = cpu.stream_encode(st, t, finish=True)
+        want.append((f, b, nb.tolist(), st.tuple()))
+    states = rc.stream_states(ns)
+    got = [b""] * ns
+    counts = [[] for _ in range(ns)]
+    cut = [sorted(rng.randint(0, len(t)) for _ in range(2)) for t in streams]
+    for part in range(3):
+        pieces = []
+        for k, t in enumerate(streams):
+            lo = 0 if part == 0 else cut[k][part - 1]
+            hi = cut[k][part] if part < 2 else len(t)
+            pieces.append(t[lo:hi])
+        lens = np.array([len(p) for p in pieces], np.int64)
+        sym_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        trip = np.array([x for p in pieces for x in p] or [(0, 0, 0)], np.uint32).reshape(-1)
+        fin = part == 2
+        caps = 12 * lens + (8 if fin else 0) + 3
+        out_off = np.concatenate([[0], np.cumsum(caps)]).astype(np.int64)
+        out = torch.full((int(out_off[-1]) + 16,), 0xEE, dtype=torch.uint8, device="cuda")
+        nb = torch.zeros(max(int(sym_off[-1]), 1), dtype=torch.uint8, device="cuda")
+        ol, fl = rc.stream_encode_batch(ctx, states, dev(trip.view(np.int32)), dev(sym_off), out,
+                                        dev(out_off), nbytes=nb, finish=fin)
+        torch.cuda.synchronize()
+        h, ol, nbh = out.cpu().numpy(), ol.cpu().numpy(), nb.cpu().numpy()
+        stt = states.cpu().numpy().view(np.uint64)
+        for k in range(ns):
+            got[k] += h[out_off[k]: out_off[k] + ol[k]].tobytes()
+            nk = int(stt[k, 4]) - len(counts[k])
+            counts[k] += nbh[sym_off[k]: sym_off[k] + nk].tolist()
+            assert (h[out_off[k] + ol[k]: out_off[k + 1]] == 0xEE).all()
+    stt = states.cpu().numpy().view(np.uint64)
+    for k in range(ns):
+        f, b, nb, tup = want[k]
+        assert got[k] == b, k
+        assert counts[k] == nb, k
+        lo, r, d, pos, n, fs = (int(x) for x in stt[k])
+        assert (lo, r, pos, n, fs & 0xFFFFFFFF, fs >> 32) == \
+            (tup[0], tup[1], tup[3], tup[4], tup[5], tup[6]), k
+
+
+def test_batch_stream_decode_split_calls_vs_oracle(ctx):
+    rng = random.Random(6)
+    ns = 120
+    na = 40
+    c = np.array([rng.choice([0, 1, rng.randint(1, 900)]) for _ in range(na)], np.uint32)
+    cum = np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.uint32)
+    total = int(c.sum())
+    codes = []
+    for k in range(ns):
+        if k % 3 == 0:  # valid streams
+            syms = [s for s in (rng.randrange(na) for _ in range(400)) if c[s]][:300]
+            codes.append(cpu.encode(c, cum, total, np.array(syms, np.uint8))[1])
+        else:  # garbage
+            codes.append(bytes(rng.randrange(256) for _ in range(rng.randint(0, 90))))
+    want = []
+    for code in codes:
+        st = cpu.Stream.fresh()
+        f, s = cpu.stream_decode(st, c, cum, total, code, 320)
+        want.append((f, s.tolist(), st.tuple()))
+    clen = np.array([len(x) for x in codes], np.int64)
+    coff = np.concatenate([[0], np.cumsum(clen)[:-1]]).astype(np.int64)
+    blob = np.frombuffer(b"".join(codes) + b"\0" * 16, np.uint8)
+    states = rc.stream_states(ns)
+    got = [[] for _ in range(ns)]
+    for part, m in enumerate((100, 0, 220)):
+        sym_off = (np.arange(ns + 1) * m).astype(np.int64)
+        syms = torch.full((ns * m + 16,), 0xEE, dtype=torch.uint8, device="cuda")
+        before = states.cpu().numpy().view(np.uint64)[:, 4].copy()
+        rc.stream_decode_batch(ctx, dev(c.view(np.int32)), dev(cum.view(np.int32)), total,
+                               states, dev(blob), dev(coff), dev(clen), syms, dev(sym_off))
+        torch.cuda.synchronize()
+        after = states.cpu().numpy().view(np.uint64)[:, 4]
+        h = syms.cpu().numpy()
+        for k in range(ns):
+            got[k] += h[k * m: k * m + int(after[k] - before[k])].tolist()
+    stt = states.cpu().numpy().view(np.uint64)
+    for k in range(ns):
+        f, s, tup = want[k]
+        assert got[k] == s, k
+        lo, r, d, pos, n, fs = (int(x) for x in stt[k])
+        assert (lo, r, d, pos, n, fs & 0xFFFFFFFF) == tup[:6], k
+
+
+def test_stream_positions_are_64_bit(ctx):
+    """A decoder whose state sits 2^33 bytes into its stream: code_off points 2^33 before the
+    window (u64 wrap-around), so only 64-bit positions address the right bytes."""
+    c = np.ones(256, np.uint32)
+    cum = np.arange(256, dtype=np.uint32)
+    rng = np.random.default_rng(9)
+    syms = rng.integers(0, 256, 500).astype(np.uint8)
+    code = cpu.encode(c, cum, 256, syms)[1]
+    # the oracle's state after Decoder::new + 100 symbols
+    st = cpu.Stream.fresh()
+    f, _ = cpu.stream_decode(st, c, cum, 256, code, 100)
+    assert f == 0
+    big = 1 << 33
+    states = rc.stream_states(1)
+    row = np.array([st.lower_bound, st.range, st.data, st.pos + big, st.n, 1 << 32], np.uint64)
+    states[0] = torch.from_numpy(row.view(np.int64)).to("cuda")
+    blob = dev(np.frombuffer(code + b"\0" * 16, np.uint8))
+    coff = np.array([(-big) & ((1 << 64) - 1)], np.uint64)
+    out = torch.zeros(400, dtype=torch.uint8, device="cuda")
+    fl = rc.stream_decode_batch(ctx, dev(c.view(np.int32)), dev(cum.view(np.int32)), 256, states,
+                                blob, dev(coff.view(np.int64)),
+                                dev(np.array([len(code) + big], np.int64)), out,
+                                dev(np.array([0, 400], np.int64)))
+    torch.cuda.synchronize()
+    assert int(fl[0]) == 0
+    assert np.array_equal(out.cpu().numpy(), syms[100:])
+    assert int(states.cpu().numpy().view(np.uint64)[0, 3]) == big + len(code)
