@@ -16,13 +16,18 @@ int main() {
     std::printf("index:%zu, c:%u, cum:%u\n", i, sd.c_freq(i), sd.cum_freq(i));
 
   rc::Encoder encoder;
-  for (size_t i : test_data) encoder.encode(sd, i);
+  uint32_t settled = 0;  // sum of encode()'s return values (encoder.rs:36)
+  for (size_t i : test_data) settled += encoder.encode(sd, i);
   const std::vector<uint8_t> code = encoder.finish();
   std::printf("output : 0x");
   for (uint8_t b : code) std::printf("%02x", b);
   std::printf("\nlength : %zubyte\n", code.size());
+  if (settled + 8 != code.size()) {
+    std::printf("byte counts FAILED\n");
+    return 1;
+  }
 
-  rc::Decoder decoder(code, test_data.size());
+  rc::Decoder decoder(code);  // Decoder::new(code): the count stays out-of-band
   std::vector<size_t> decodeds;
   for (size_t k = 0; k < test_data.size(); ++k) decodeds.push_back(decoder.decode(sd));
   if (decodeds != test_data) {

@@ -148,6 +148,23 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
                          const uint64_t* code_off, const uint64_t* code_len, uint8_t* syms_out,
                          const uint64_t* sym_off, uint32_t n_chunks, uint32_t* flags);
 
+/* ---- several devices of one node from one host thread (the rc_*_multi entry points) ----
+ * rc_encode_host / rc_decode_host over a list of contexts (one per device; two contexts on one
+ * device also work): the chunks are cut into n_ctx contiguous ranges of about equal input
+ * bytes, coded concurrently (one host thread per context).  Chunks are independent streams
+ * (a fresh Encoder each, encoder.rs:48-55), so there is no data-path exchange between devices:
+ * every device reads its range of the caller's buffers and writes its chunks' results in place.
+ * models[i] is the model as created on ctxs[i]'s device (identical tables).  Returns the first
+ * failing status, RC_E_CHUNK when a chunk is flagged, else RC_OK.                             */
+rc_status rc_encode_host_multi(rc_ctx* const* ctxs, const rc_model* const* models, uint32_t n_ctx,
+                               const uint8_t* syms, const uint64_t* sym_off, uint32_t n_chunks,
+                               uint8_t* out, const uint64_t* out_off, uint64_t* out_len,
+                               uint32_t* flags);
+rc_status rc_decode_host_multi(rc_ctx* const* ctxs, const rc_model* const* models, uint32_t n_ctx,
+                               const uint8_t* code, const uint64_t* code_off,
+                               const uint64_t* code_len, uint8_t* syms_out,
+                               const uint64_t* sym_off, uint32_t n_chunks, uint32_t* flags);
+
 /* ---- resumable streams: the reference's per-call Encoder / Decoder (any PModel) ----
  * The batch entry points code whole chunks against one table.  The reference instead reads the
  * model on EVERY call — Encoder::encode takes (c_freq(i), cum_freq(i), total_freq()) of the

@@ -3,9 +3,12 @@
 //
 //   trait PModel            (src/pmodel.rs:4-41)         -> rc::PModel (abstract class)
 //   FreqTable example model (examples/sample_impl.rs)    -> rc::FreqTable
-//   Encoder::new/encode/finish (src/encoder.rs:14-46)    -> rc::Encoder (one stream, staged;
-//                                                           finish() encodes on the GPU)
-//   Decoder::new/decode       (src/decoder.rs:14-54)     -> rc::Decoder (count out-of-band)
+//   RangeCoder accessors      (src/range_coder.rs:26-146) -> rc::RangeCoder (a state snapshot)
+//   Encoder::new/encode/peek_code/finish, pub range_coder
+//                             (src/encoder.rs:7-55)       -> rc::Encoder (model read per call;
+//                                                           encode() returns a ByteCount)
+//   Decoder::new/decode/range_coder/data
+//                             (src/decoder.rs:6-55)       -> rc::Decoder (model read per call)
 //   error::RangeCoderError     (src/error.rs:3-13)       -> rc::RangeCoderError (exception)
 //   (new) batch API                                      -> rc::encode_chunks / decode_chunks
 //
@@ -14,6 +17,7 @@
 #ifndef RANGE_CODER_AMD_HPP
 #define RANGE_CODER_AMD_HPP
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <memory>
@@ -48,6 +52,9 @@ inline std::string flag_string(uint32_t f) {
   if (f & RC_F_CAPACITY) s += "CAPACITY|";
   if (f & RC_F_TRUNCATED) s += "TRUNCATED|";
   if (f & RC_F_CORRUPT) s += "CORRUPT|";
+  if (f & RC_F_TOO_LONG) s += "TOO_LONG|";
+  if (f & RC_F_BAD_MODEL) s += "BAD_MODEL|";
+  if (f & RC_F_FINISHED) s += "FINISHED|";
   if (!s.empty()) s.pop_back();
   return s;
 }
@@ -231,53 +238,237 @@ inline std::vector<std::vector<uint8_t>> decode_chunks(
   return res;
 }
 
-// Encoder (src/encoder.rs:7-55) for one stream: encode() stages the symbol (it cannot return
-// the per-symbol byte count of encoder.rs:36 because nothing is coded before finish()).
-class Encoder {
+// RangeCoder (src/range_coder.rs:7-146): the public accessors of a coder state (a snapshot: a
+// stream's state lives with its GPU calls, rc_stream_state)
+class RangeCoder {
  public:
-  Encoder() = default;
-  static Encoder new_() { return Encoder(); }
-  void encode(const PModel& pm, size_t index) {
-    if (pm_ && pm_ != &pm) throw RangeCoderError("one static model per staged stream");
-    pm_ = &pm;
-    if (index >= pm.alphabet_count() || index > 255)
-      throw RangeCoderError("symbol index outside the alphabet", RC_E_CHUNK, RC_F_BAD_SYMBOL);
-    syms_.push_back((uint8_t)index);
+  static constexpr uint64_t TOP8 = 1ull << 56;   // range_coder.rs:23
+  static constexpr uint64_t TOP16 = 1ull << 48;  // range_coder.rs:24
+  RangeCoder() = default;                         // Default (:13-20)
+  RangeCoder(uint64_t lower_bound, uint64_t range) : low_(lower_bound), range_(range) {}
+  static RangeCoder new_() { return RangeCoder(); }
+  uint64_t lower_bound() const { return low_; }  // :30-32
+  uint64_t range() const { return range_; }      // :33-35
+  uint64_t range_par_total(uint32_t total_freq) const {  // :38-40
+    if (total_freq == 0) throw RangeCoderError("range_par_total: attempt to divide by zero");
+    return range_ / total_freq;
   }
-  // Encoder::finish (encoder.rs:40-46): the stream, 8 + sum of per-symbol bytes long
-  std::vector<uint8_t> finish(Context& ctx = Context::default_context()) {
-    if (!pm_) return std::vector<uint8_t>(8, 0);  // lower_bound == 0, 8 bytes
-    Model m(ctx, *pm_);
-    return encode_chunks(m, {syms_})[0];
+  uint64_t upper_bound() const {  // :138-146
+    const uint64_t u = low_ + range_;
+    if (u < low_) throw RangeCoderError("UpperBoundOverflow");
+    return u;
   }
+  bool operator==(const RangeCoder& o) const { return low_ == o.low_ && range_ == o.range_; }
 
  private:
-  const PModel* pm_ = nullptr;
-  std::vector<uint8_t> syms_;
+  uint64_t low_ = 0, range_ = ~0ull;
 };
 
-// Decoder (src/decoder.rs:6-55) for one stream of n_symbols symbols.
-class Decoder {
+inline void throw_flags(uint32_t f, const std::string& where) {
+  if (f) throw RangeCoderError(where + ": " + flag_string(f), RC_E_CHUNK, f);
+}
+
+class Encoder;
+
+// Encoder::encode's return value (encoder.rs:34-36: the bytes that symbol settled).  Symbols
+// are staged and coded on the GPU in batches; converting to uint32_t flushes them if needed.
+// Valid while its Encoder lives.
+class ByteCount {
  public:
-  Decoder(std::vector<uint8_t> code, uint64_t n_symbols) : code_(std::move(code)), n_(n_symbols) {
-    if (code_.size() < 8)  // Decoder::new panics (decoder.rs:21, :33)
-      throw RangeCoderError("code shorter than 8 bytes", RC_E_CHUNK, RC_F_TRUNCATED);
+  ByteCount(Encoder* e, uint64_t i) : e_(e), i_(i) {}
+  operator uint32_t() const;
+
+ private:
+  Encoder* e_;
+  uint64_t i_;
+};
+
+// Encoder (src/encoder.rs:7-55) for one stream, with the reference's per-call semantics:
+// encode() reads (c_freq(index), cum_freq(index), total_freq()) at that call
+// (encoder.rs:24-31), so a PModel the caller changes between calls is coded exactly as the
+// reference codes it.  The staged triples are coded by the resumable stream kernel
+// (rc_stream_encode_host) when a result is needed: peek_code(), range_coder(), finish(), a
+// ByteCount's value, or every 2^20 symbols.  No length limit.
+class Encoder {
+ public:
+  static constexpr size_t FLUSH_AT = 1u << 20;
+  explicit Encoder(Context& ctx = Context::default_context()) : ctx_(&ctx) {}
+  Encoder(const Encoder&) = delete;
+  Encoder& operator=(const Encoder&) = delete;
+  static Encoder new_() { return Encoder(); }  // encoder.rs:14-16
+
+  ByteCount encode(const PModel& pm, size_t index) {  // encoder.rs:24-37
+    if (finished_) throw RangeCoderError("encode after finish", RC_E_CHUNK, RC_F_FINISHED);
+    if (index >= pm.alphabet_count())  // sample_impl.rs:19: get(index).unwrap() panics
+      throw RangeCoderError("symbol index outside the alphabet", RC_E_CHUNK, RC_F_BAD_SYMBOL);
+    const uint32_t c = pm.c_freq(index), cum = pm.cum_freq(index), total = pm.total_freq();
+    if (c == 0)  // range_coder.rs:83-85 would never terminate
+      throw RangeCoderError("encode: c_freq == 0", RC_E_CHUNK, RC_F_ZERO_FREQ);
+    if (total == 0)  // range_coder.rs:38-40 divides by zero
+      throw RangeCoderError("encode: total_freq == 0", RC_E_CHUNK, RC_F_BAD_MODEL);
+    trip_.insert(trip_.end(), {c, cum, total});
+    const uint64_t i = staged0_ + trip_.size() / 3 - 1;
+    if (trip_.size() >= 3 * FLUSH_AT) flush(false);
+    return ByteCount(this, i);
   }
-  size_t decode(const PModel& pm, Context& ctx = Context::default_context()) {
-    if (!decoded_) {
-      Model m(ctx, pm);
-      out_ = decode_chunks(m, {code_}, {n_})[0];
-      decoded_ = true;
-    }
-    if (pos_ >= out_.size()) throw RangeCoderError("more decode() calls than n_symbols");
-    return out_[pos_++];
+  const std::vector<uint8_t>& peek_code() {  // encoder.rs:18-20
+    flush(false);
+    return code_;
+  }
+  RangeCoder range_coder() {  // the pub field of encoder.rs:8 (a snapshot)
+    flush(false);
+    return RangeCoder(st_.lower_bound, st_.range);
+  }
+  std::vector<uint8_t> finish() {  // encoder.rs:40-46
+    if (finished_) throw RangeCoderError("finish twice", RC_E_CHUNK, RC_F_FINISHED);
+    flush(true);
+    finished_ = true;
+    return code_;
+  }
+  uint32_t count(uint64_t i) {
+    if (i >= staged0_) flush(false);
+    if (i >= counts_.size()) throw RangeCoderError("symbol not coded (an earlier one failed)");
+    return counts_[i];
   }
 
  private:
-  std::vector<uint8_t> code_, out_;
-  uint64_t n_;
-  size_t pos_ = 0;
-  bool decoded_ = false;
+  void flush(bool finish) {
+    const uint64_t n = trip_.size() / 3;
+    if (n == 0 && !finish) return;
+    throw_flags(st_.flags, "encode");
+    const uint64_t cap = RC_STREAM_MAX_BYTES(n, finish);
+    std::vector<uint8_t> out(cap ? cap : 1), nb(n ? n : 1);
+    uint64_t len = 0;
+    uint32_t fl = 0;
+    const uint64_t n0 = st_.n;
+    const rc_status s = rc_stream_encode_host(ctx_->get(), &st_, trip_.data(), n, out.data(), cap,
+                                              &len, nb.data(), finish ? 1u : 0u, &fl);
+    if (s != RC_OK && s != RC_E_CHUNK) check(s, "rc_stream_encode_host");
+    code_.insert(code_.end(), out.begin(), out.begin() + len);
+    counts_.insert(counts_.end(), nb.begin(), nb.begin() + (st_.n - n0));
+    staged0_ += n;
+    trip_.clear();
+    throw_flags(fl, "encode (symbol " + std::to_string(st_.n) + ")");
+  }
+  Context* ctx_;
+  rc_stream_state st_ = RC_STREAM_STATE_INIT;
+  std::vector<uint8_t> code_, counts_;
+  std::vector<uint32_t> trip_;
+  uint64_t staged0_ = 0;
+  bool finished_ = false;
+};
+
+inline ByteCount::operator uint32_t() const { return e_->count(i_); }
+
+// Decoder (src/decoder.rs:6-55) for one stream, with the reference's per-call semantics:
+// decode() reads the model's table at that call and decodes with FreqTable::find_index's
+// binary search and param_update (sample_impl.rs:27-45, decoder.rs:38-54) on the GPU
+// (rc_stream_decode_host).  Symbols are decoded ahead in blocks that double while the table
+// stays the same; when the caller's table changes the state at that symbol is re-derived, so
+// every symbol is decoded with the table held at its call.  The user's find_index is not
+// called (for a table whose (c, cum) intervals tile [0, total) it equals the binary search).
+class Decoder {
+ public:
+  static constexpr uint64_t MAX_BLOCK = 1u << 20;
+  // Decoder::new (decoder.rs:14-23): a code shorter than 8 bytes panics there
+  explicit Decoder(std::vector<uint8_t> code, Context& ctx = Context::default_context())
+      : Decoder(std::move(code), ~0ull, ctx) {}
+  // n_symbols: the out-of-band count (sample_impl.rs:113-120); only bounds the decode-ahead
+  Decoder(std::vector<uint8_t> code, uint64_t n_symbols, Context& ctx = Context::default_context())
+      : ctx_(&ctx), code_(std::move(code)), limit_(n_symbols) {
+    if (code_.size() < 8)
+      throw RangeCoderError("code shorter than 8 bytes", RC_E_CHUNK, RC_F_TRUNCATED);
+    Table t{{1}, {0}, 1};
+    run(start_, t, 0, nullptr);  // prime the data window
+    end_ = start_;
+  }
+  static Decoder new_(std::vector<uint8_t> code) { return Decoder(std::move(code)); }
+
+  size_t decode(const PModel& pm) {  // decoder.rs:38-54
+    Table t = table_of(pm);
+    const bool same = have_ && t == sig_;
+    if (same && bpos_ < buf_.size()) {
+      ++taken_;
+      return buf_[bpos_++];
+    }
+    if (same && err_) throw_flags(err_, "decode (symbol " + std::to_string(taken_) + ")");
+    block_ = (same && bpos_ == buf_.size()) ? std::min<uint64_t>(2 * block_, MAX_BLOCK) : 1;
+    rc_stream_state st = here();
+    uint64_t n = block_;
+    if (limit_ != ~0ull) n = std::max<uint64_t>(1, std::min<uint64_t>(n, limit_ - taken_));
+    const rc_stream_state start = st;
+    std::vector<uint8_t> out(n);
+    const uint32_t fl = run(st, t, n, out.data());
+    out.resize(st.n - start.n);
+    start_ = start;
+    end_ = st;
+    buf_ = std::move(out);
+    bpos_ = 0;
+    sig_ = std::move(t);
+    have_ = true;
+    err_ = fl;
+    if (buf_.empty()) throw_flags(fl, "decode (symbol " + std::to_string(taken_) + ")");
+    ++taken_;
+    return buf_[bpos_++];
+  }
+  RangeCoder range_coder() {  // decoder.rs:24-26 (a snapshot)
+    const rc_stream_state st = here();
+    return RangeCoder(st.lower_bound, st.range);
+  }
+  uint64_t data() { return here().data; }  // decoder.rs:27-29
+
+ private:
+  struct Table {
+    std::vector<uint32_t> c, cum;
+    uint32_t total;
+    bool operator==(const Table& o) const { return total == o.total && c == o.c && cum == o.cum; }
+  };
+  static Table table_of(const PModel& pm) {
+    Table t;
+    const size_t n = pm.alphabet_count();
+    t.c.resize(n);
+    t.cum.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      t.c[i] = pm.c_freq(i);
+      t.cum[i] = pm.cum_freq(i);
+    }
+    t.total = pm.total_freq();
+    return t;
+  }
+  uint32_t run(rc_stream_state& st, const Table& t, uint64_t n, uint8_t* out) {
+    uint32_t fl = 0;
+    uint8_t dummy = 0;
+    const rc_status s = rc_stream_decode_host(ctx_->get(), t.c.data(), t.cum.data(),
+                                              (uint32_t)t.c.size(), t.total, &st, code_.data(),
+                                              code_.size(), out ? out : &dummy, n, &fl);
+    if (s != RC_OK && s != RC_E_CHUNK) check(s, "rc_stream_decode_host");
+    return fl;
+  }
+  // the state at the current symbol (re-derived inside a block, which then starts here)
+  rc_stream_state here() {
+    if (bpos_ == 0) return start_;
+    if (bpos_ == buf_.size()) {
+      rc_stream_state st = end_;
+      st.flags = 0;
+      return st;
+    }
+    rc_stream_state st = start_;
+    std::vector<uint8_t> tmp(bpos_);
+    run(st, sig_, bpos_, tmp.data());
+    start_ = st;
+    buf_.erase(buf_.begin(), buf_.begin() + bpos_);
+    bpos_ = 0;
+    return st;
+  }
+  Context* ctx_;
+  std::vector<uint8_t> code_, buf_;
+  uint64_t limit_;
+  rc_stream_state start_ = RC_STREAM_STATE_INIT, end_ = RC_STREAM_STATE_INIT;
+  size_t bpos_ = 0;
+  Table sig_;
+  bool have_ = false;
+  uint32_t err_ = 0;
+  uint64_t block_ = 1, taken_ = 0;
 };
 
 }  // namespace rc

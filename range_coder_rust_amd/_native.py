@@ -35,6 +35,7 @@ EXPORTS = (
     "rc_decode_host", "rc_synth_fill", "rc_histogram", "rc_quantize_counts", "rc_ideal_bits",
     "rc_container_pack", "rc_container_info_parse", "rc_container_offsets",
     "rc_stream_encode", "rc_stream_decode", "rc_stream_encode_host", "rc_stream_decode_host",
+    "rc_encode_host_multi", "rc_decode_host_multi",
 )
 RC_E_BAD_CONTAINER = -6
 RC_E_CAPACITY = -7
@@ -119,6 +120,8 @@ def load():
                                         _U32, ctypes.POINTER(_U32)]
     L.rc_stream_decode_host.argtypes = [_P, _P, _P, _U32, _U32, SP, _P, _U64, _P, _U64,
                                         ctypes.POINTER(_U32)]
+    L.rc_encode_host_multi.argtypes = [_P, _P, _U32, _P, _P, _U32, _P, _P, _P, _P]
+    L.rc_decode_host_multi.argtypes = [_P, _P, _U32, _P, _P, _P, _P, _P, _U32, _P]
     for name in EXPORTS:
         if name not in ("rc_status_string", "rc_last_error"):
             getattr(L, name).restype = _I

@@ -27,7 +27,7 @@ __all__ = [
     "Context", "StaticModel", "PModel", "FreqTable", "Encoder", "Decoder", "RangeCoderError",
     "ZeroFrequencyError", "BadSymbolError", "TruncatedStreamError", "CorruptStreamError",
     "CapacityError", "ChunkTooLongError", "BadModelError", "FinishedError", "RangeCoder",
-    "ByteCount", "stream_states", "stream_encode_batch", "stream_decode_batch", "encode_batch", "decode_batch", "encode_chunks", "decode_chunks",
+    "ByteCount", "encode_host_multi", "decode_host_multi", "stream_states", "stream_encode_batch", "stream_decode_batch", "encode_batch", "decode_batch", "encode_chunks", "decode_chunks",
     "default_context", "flag_names", "slot_capacity",
 ]
 
@@ -885,4 +885,57 @@ def decode_host(model, code, code_off, code_len, sym_off, out=None):
                                  _np_ptr(flags))
     if rc not in (N.RC_OK, N.RC_E_CHUNK):
         N.check(rc, "rc_decode_host")
+    return syms, flags[:n]
+
+
+# ----------------------------------------------------------------------------- several devices
+def _handles(models):
+    ctxs = (ctypes.c_void_p * len(models))(*[m.ctx.handle.value for m in models])
+    hs = (ctypes.c_void_p * len(models))(*[m.handle.value for m in models])
+    return ctxs, hs
+
+
+def encode_host_multi(models, syms, sym_off, out_off, out=None):
+    """rc_encode_host_multi: encode_host over several devices at once.  models: one model per
+    device (context), e.g. [StaticModel(c, cum, total, ctx=Context(d)) for d in devices]; the
+    chunks are split into contiguous ranges of about equal bytes, one per model.  Returns
+    (out, out_len, flags) like encode_host."""
+    if not models:
+        raise ValueError("need at least one model")
+    syms = np.ascontiguousarray(syms, dtype=np.uint8)
+    sym_off = np.ascontiguousarray(sym_off, dtype=np.uint64)
+    out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
+    n = len(sym_off) - 1
+    if out is None:
+        out = np.empty(int(out_off[-1]), np.uint8)
+    out_len = np.zeros(max(n, 1), np.uint64)
+    flags = np.zeros(max(n, 1), np.uint32)
+    ctxs, hs = _handles(models)
+    rc = models[0].ctx._lib.rc_encode_host_multi(ctxs, hs, len(models), _np_ptr(syms),
+                                                 _np_ptr(sym_off), n, _np_ptr(out),
+                                                 _np_ptr(out_off), _np_ptr(out_len),
+                                                 _np_ptr(flags))
+    if rc not in (N.RC_OK, N.RC_E_CHUNK):
+        N.check(rc, "rc_encode_host_multi")
+    return out, out_len[:n], flags[:n]
+
+
+def decode_host_multi(models, code, code_off, code_len, sym_off, out=None):
+    """rc_decode_host_multi: decode_host over several devices at once.  Returns (syms, flags)."""
+    if not models:
+        raise ValueError("need at least one model")
+    code = np.ascontiguousarray(code, dtype=np.uint8)
+    code_off = np.ascontiguousarray(code_off, dtype=np.uint64)
+    code_len = np.ascontiguousarray(code_len, dtype=np.uint64)
+    sym_off = np.ascontiguousarray(sym_off, dtype=np.uint64)
+    n = len(sym_off) - 1
+    syms = np.empty(int(sym_off[-1]), np.uint8) if out is None else out
+    flags = np.zeros(max(n, 1), np.uint32)
+    ctxs, hs = _handles(models)
+    rc = models[0].ctx._lib.rc_decode_host_multi(ctxs, hs, len(models), _np_ptr(code),
+                                                 _np_ptr(code_off), _np_ptr(code_len),
+                                                 _np_ptr(syms), _np_ptr(sym_off), n,
+                                                 _np_ptr(flags))
+    if rc not in (N.RC_OK, N.RC_E_CHUNK):
+        N.check(rc, "rc_decode_host_multi")
     return syms, flags[:n]

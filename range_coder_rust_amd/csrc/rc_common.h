@@ -63,6 +63,13 @@ static __device__ __forceinline__ void gstore32(uint8_t* p, u32 v) { *(g_u32*)p 
 static __device__ __forceinline__ void gstore64(uint8_t* p, u64 v) { *(g_u64*)p = v; }
 static __device__ __forceinline__ void gstore128(uint8_t* p, u32x4 v) { *(g_u32x4*)p = v; }
 
+// A pinned host buffer of at least `bytes` (<= 1 MiB) for this host thread, grown on demand
+// (rc_kernels.hip).  Host <-> device transfers of small control data go through it: async
+// copies to and from pageable memory returned wrong bytes intermittently on this stack
+// (DESIGN.md §6), pinned ones are plain stream-ordered DMA.  Contents are the caller's until
+// its next call on the same thread.
+void* rc_pinned_scratch_(size_t bytes);
+
 // Adaptive order-0 model parameters (rc_model_create_adaptive)
 struct AdaptParams {
   u32 n;      // alphabet size (1..256)

@@ -305,7 +305,12 @@ rc_status rc_container_pack(rc_ctx* ctx, const rc_model* m, const uint8_t* slots
   u64* tmp = soff + (n_chunks + 1);
   hipError_t e = device_scan(s, code_len_dev, n_chunks, SCAN_SRC_PAD16, 0, payload_off, doff, tmp);
   if (e == hipSuccess) e = device_scan(s, sym_off_dev, n_chunks, SCAN_SRC_DIFF, 0, 0, soff, tmp);
-  u64 ends[2] = {payload_off, 0};
+  // small read-backs and the header go through pinned memory: [0, 16) ends, [64, ...) header
+  char* pin = (char*)rc_pinned_scratch_(64 + RC_CONTAINER_HEADER_BYTES + 1024 + 16);
+  if (!pin) return RC_E_DEVICE;
+  u64* ends = (u64*)pin;
+  ends[0] = payload_off;
+  ends[1] = 0;
   if (e == hipSuccess) e = hipMemcpyAsync(&ends[0], doff + n_chunks, 8, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipMemcpyAsync(&ends[1], soff + n_chunks, 8, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -329,7 +334,8 @@ rc_status rc_container_pack(rc_ctx* ctx, const rc_model* m, const uint8_t* slots
   put64(head + 48, total_bytes - payload_off);
   if (kind == 0)
     for (u32 i = 0; i < nsym; ++i) put32(head + RC_CONTAINER_HEADER_BYTES + 4 * i, c_host[i]);
-  if (hipMemcpyAsync(dst_dev, head, index_off, hipMemcpyHostToDevice, s) != hipSuccess)
+  memcpy(pin + 64, head, index_off);
+  if (hipMemcpyAsync(dst_dev, pin + 64, index_off, hipMemcpyHostToDevice, s) != hipSuccess)
     return RC_E_DEVICE;
   if (n_chunks) {
     int cus = 0;
@@ -340,7 +346,8 @@ rc_status rc_container_pack(rc_ctx* ctx, const rc_model* m, const uint8_t* slots
                        reinterpret_cast<u64*>(dst_dev + index_off));
     if (hipGetLastError() != hipSuccess) return RC_E_DEVICE;
   }
-  // the header lives on this stack frame: wait for its copy (and free the scratch in order)
+  // the pinned staging is reused by this thread's next call: wait for its copy (and free the
+  // scratch in order)
   return hipStreamSynchronize(s) == hipSuccess ? RC_OK : RC_E_DEVICE;
 }
 
@@ -373,13 +380,15 @@ rc_status rc_container_offsets(rc_ctx* ctx, const uint8_t* container_dev,
   if (e == hipSuccess) e = device_scan(s, index, n, SCAN_SRC_STRIDE2, 0, 0, sym_off_dev, tmp);
   if (e == hipSuccess && n)
     e = hipMemcpyAsync(code_off_dev, coff, 8ull * n, hipMemcpyDeviceToDevice, s);
-  u64 ends[2] = {0, 0};
-  u32 hbad = 0;
+  u64* ends = (u64*)rc_pinned_scratch_(24);  // small read-backs through pinned memory
+  if (!ends) return RC_E_DEVICE;
+  ends[0] = ends[1] = ends[2] = 0;
   if (e == hipSuccess) e = hipMemcpyAsync(&ends[0], coff + n, 8, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess && n) e = hipMemcpyAsync(&ends[1], sym_off_dev + n, 8, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(&ends[2], bad, 4, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return RC_E_DEVICE;
+  const u32 hbad = (u32)ends[2];
   // the index must describe exactly the payload the header announces
   if (hbad || ends[0] != info->payload_off + info->payload_bytes || ends[1] != info->n_syms)
     return RC_E_BAD_CONTAINER;

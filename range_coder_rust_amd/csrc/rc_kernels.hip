@@ -102,7 +102,29 @@ rc_status launch_status() {
   return e == hipSuccess ? RC_OK : device_error(e, "kernel launch");
 }
 
+struct PinnedScratch {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~PinnedScratch() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+thread_local PinnedScratch t_pinned;
+
 }  // namespace
+
+void* rc_pinned_scratch_(size_t bytes) {
+  if (bytes > (1u << 20)) return nullptr;
+  if (t_pinned.cap < bytes) {
+    if (t_pinned.p) (void)hipHostFree(t_pinned.p);
+    t_pinned.p = nullptr;
+    t_pinned.cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 1u << 16);
+    if (hipHostMalloc(&t_pinned.p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    t_pinned.cap = cap;
+  }
+  return t_pinned.p;
+}
 
 extern "C" {
 
@@ -160,11 +182,13 @@ rc_status rc_ctx_create(int device, rc_ctx** out) {
 }
 
 void rc_stream_release_(const rc_ctx* ctx);  // rc_stream.hip: the cached host pipeline
+void rc_resume_release_(const rc_ctx* ctx);  // rc_resume.hip: the stream API's staging
 
 rc_status rc_ctx_destroy(rc_ctx* ctx) {
   if (!ctx) return RC_E_ARG;
   DeviceGuard g(ctx->device);
   rc_stream_release_(ctx);
+  rc_resume_release_(ctx);
   (void)hipStreamSynchronize(ctx->own);
   (void)hipStreamSynchronize(ctx->cur);
   (void)hipFree(ctx->inv);
@@ -404,7 +428,10 @@ rc_status rc_synth_fill(rc_ctx* ctx, uint64_t seed, const uint8_t* inv_cdf_host,
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
   const uint8_t* dinv = ctx->inv;
-  hipError_t e = hipMemcpyAsync(ctx->inv, inv_cdf_host, 65536, hipMemcpyHostToDevice, ctx->cur);
+  void* pin = rc_pinned_scratch_(65536);
+  if (!pin) return RC_E_DEVICE;
+  memcpy(pin, inv_cdf_host, 65536);
+  hipError_t e = hipMemcpyAsync(ctx->inv, pin, 65536, hipMemcpyHostToDevice, ctx->cur);
   if (e != hipSuccess) return device_error(e, "rc_synth_fill copy");
   if ((chunk_len & 15) == 0 && ((uintptr_t)syms_dev & 15) == 0) {
     const u64 words = (chunk_len >> 4) * (u64)n_chunks;
@@ -416,7 +443,7 @@ rc_status rc_synth_fill(rc_ctx* ctx, uint64_t seed, const uint8_t* inv_cdf_host,
                        seed, dinv, syms_dev, chunk_len, n_chunks);
   }
   rc_status st = launch_status();
-  // the host table may be freed once the call returns: wait for the copy
+  // the pinned staging is reused by this thread's next call: wait for the copy
   if (st == RC_OK && (e = hipStreamSynchronize(ctx->cur)) != hipSuccess)
     return device_error(e, "rc_synth_fill sync");
   return st;

@@ -225,14 +225,20 @@ rc_status rc_ideal_bits(rc_ctx* ctx, const uint32_t* c_host, uint32_t n_symbols,
   DevSet g(dev);
   double* d = nullptr;
   if (hipMallocAsync((void**)&d, sizeof icl, s) != hipSuccess) return RC_E_DEVICE;
-  if (hipMemcpyAsync(d, icl, sizeof icl, hipMemcpyHostToDevice, s) != hipSuccess) {
+  void* pin = rc_pinned_scratch_(sizeof icl);
+  if (!pin) {
+    (void)hipFreeAsync(d, s);
+    return RC_E_DEVICE;
+  }
+  memcpy(pin, icl, sizeof icl);
+  if (hipMemcpyAsync(d, pin, sizeof icl, hipMemcpyHostToDevice, s) != hipSuccess) {
     (void)hipFreeAsync(d, s);
     return RC_E_DEVICE;
   }
   hipLaunchKernelGGL(k_ideal_bits, dim3((n_chunks + HWG - 1) / HWG), dim3(HWG), 0, s, d,
                      chunk_hist, n_chunks, bits);
   const bool ok = hipGetLastError() == hipSuccess;
-  // icl lives on the host stack: wait for the copy before returning
+  // the pinned staging is reused by this thread's next call: wait for the copy
   const bool fr = hipFreeAsync(d, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
   return ok && fr ? RC_OK : RC_E_DEVICE;
 }

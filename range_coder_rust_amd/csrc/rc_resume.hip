@@ -22,6 +22,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 #define RWG 64
 #define TOP8 (1ull << 56)  // range_coder.rs:23
@@ -239,20 +241,43 @@ struct Dev {
   }
 };
 
-// stream-ordered device scratch for the host variants, freed on every return path
-struct Scratch {
-  hipStream_t s;
-  void* p = nullptr;
-  Scratch(hipStream_t s_, size_t n) : s(s_) {
-    if (hipMallocAsync(&p, std::max<size_t>(n, 16), s) != hipSuccess) p = nullptr;
-  }
-  ~Scratch() {
-    if (p) {
-      (void)hipFreeAsync(p, s);
-      (void)hipStreamSynchronize(s);
-    }
-  }
+// The host variants' staging: one pinned host block and its device mirror per context, grown on
+// demand and kept until rc_ctx_destroy.  Every transfer is one DMA between the two (pageable
+// caller memory is only touched by host memcpy), so copies and the kernel are plainly ordered
+// on the context's stream.  (Small async copies to and from pageable memory returned wrong
+// bytes intermittently on this stack; pinned staging is also the faster path.)  A context is
+// used by one host thread at a time (include/range_coder.h), so its block needs no lock.
+struct Stage {
+  char* host = nullptr;
+  char* dev = nullptr;
+  size_t cap = 0;
 };
+std::mutex g_stage_mu;
+std::unordered_map<const rc_ctx*, Stage> g_stages;
+
+char* stage_acquire(const rc_ctx* ctx, size_t bytes, char** dev) {
+  Stage* st;
+  {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    st = &g_stages[ctx];
+  }
+  if (st->cap < bytes) {
+    if (st->host) (void)hipHostFree(st->host);
+    if (st->dev) (void)hipFree(st->dev);
+    st->host = st->dev = nullptr;
+    st->cap = 0;
+    const size_t cap = std::max<size_t>(bytes + bytes / 2, 1u << 16);
+    if (hipHostMalloc((void**)&st->host, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (hipMalloc((void**)&st->dev, cap) != hipSuccess) {
+      (void)hipHostFree(st->host);
+      st->host = nullptr;
+      return nullptr;
+    }
+    st->cap = cap;
+  }
+  *dev = st->dev;
+  return st->host;
+}
 
 }  // namespace
 
@@ -309,36 +334,38 @@ rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint3
     return RC_E_CAPACITY;
   }
   Dev g(dev);
-  // layout: state | offsets (4 x u64) | out_len | flags | triples | nbytes | out
+  // block: state | offsets (4 x u64) | out_len | flags | triples || nbytes | out
   const size_t o_off = 64, o_len = o_off + 32, o_fl = o_len + 16, o_tr = o_fl + 16;
   const size_t o_nb = o_tr + ((12 * n + 15) & ~15ull), o_out = o_nb + ((n + 15) & ~15ull);
-  Scratch sc(s, o_out + need);
-  if (!sc.p) return RC_E_DEVICE;
-  char* d = (char*)sc.p;
+  char* d = nullptr;
+  char* h = stage_acquire(ctx, o_out + need, &d);
+  if (!h) return RC_E_DEVICE;
+  memcpy(h, state, sizeof *state);
   const u64 offs[4] = {0, n, 0, need};  // sym_off[0..1], out_off[0..1]
-  bool ok = hipMemcpyAsync(d, state, sizeof *state, hipMemcpyHostToDevice, s) == hipSuccess &&
-            hipMemcpyAsync(d + o_off, offs, sizeof offs, hipMemcpyHostToDevice, s) == hipSuccess &&
-            (!n || hipMemcpyAsync(d + o_tr, triples, 12 * n, hipMemcpyHostToDevice, s) ==
-                       hipSuccess);
-  if (!ok) return RC_E_DEVICE;
+  memcpy(h + o_off, offs, sizeof offs);
+  if (n) memcpy(h + o_tr, triples, 12 * n);
+  if (hipMemcpyAsync(d, h, o_nb, hipMemcpyHostToDevice, s) != hipSuccess) return RC_E_DEVICE;
   hipLaunchKernelGGL(k_stream_encode, dim3(1), dim3(RWG), 0, s, (rc_stream_state*)d,
                      (const u32*)(d + o_tr), (const u64*)(d + o_off), 1u, (uint8_t*)(d + o_out),
                      (const u64*)(d + o_off + 16), (u64*)(d + o_len),
                      nbytes ? (uint8_t*)(d + o_nb) : (uint8_t*)nullptr, finish,
                      (u32*)(d + o_fl));
   if (hipGetLastError() != hipSuccess) return RC_E_DEVICE;
+  // state, out_len and flags, then the new bytes and counts
+  if (hipMemcpyAsync(h, d, o_tr, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(h + o_nb, d + o_nb, o_out + need - o_nb, hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return RC_E_DEVICE;
   rc_stream_state nst;
-  u32 fl = 0;
-  ok = hipMemcpyAsync(&nst, d, sizeof nst, hipMemcpyDeviceToHost, s) == hipSuccess &&
-       hipMemcpyAsync(&fl, d + o_fl, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-       hipStreamSynchronize(s) == hipSuccess;
-  if (!ok) return RC_E_DEVICE;
-  const u64 w = nst.pos - state->pos;
-  if (w && hipMemcpyAsync(out, d + o_out, w, hipMemcpyDeviceToHost, s) != hipSuccess)
-    return RC_E_DEVICE;
-  if (nbytes && n && hipMemcpyAsync(nbytes, d + o_nb, n, hipMemcpyDeviceToHost, s) != hipSuccess)
-    return RC_E_DEVICE;
-  if (hipStreamSynchronize(s) != hipSuccess) return RC_E_DEVICE;
+  memcpy(&nst, h, sizeof nst);
+  u64 w;
+  u32 fl;
+  memcpy(&w, h + o_len, 8);
+  memcpy(&fl, h + o_fl, 4);
+  if (w > need) return RC_E_DEVICE;
+  if (w) memcpy(out, h + o_out, w);
+  if (nbytes && n) memcpy(nbytes, h + o_nb, nst.n - state->n);
   *state = nst;
   *out_len = w;
   if (flags_out) *flags_out = fl;
@@ -360,43 +387,57 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
   if (p0 > code_len) return RC_E_ARG;
   const u64 wlen = std::min<u64>(code_len - p0, (state->stage == 0 ? 8 : 0) + 12 * n);
   Dev g(dev);
-  // layout: state | offsets: code_off, code_len, sym_off[0..1] | flags | c | cum | window | syms
+  // block: state | offsets: code_off, code_len, sym_off[0..1] | flags | c | cum | window || syms
   const size_t o_off = 64, o_fl = o_off + 32, o_c = o_fl + 16, o_cum = o_c + 1024;
   const size_t o_win = o_cum + 1024, o_sym = o_win + ((wlen + 15) & ~15ull);
-  Scratch sc(s, o_sym + n);
-  if (!sc.p) return RC_E_DEVICE;
-  char* d = (char*)sc.p;
+  char* d = nullptr;
+  char* h = stage_acquire(ctx, o_sym + n, &d);
+  if (!h) return RC_E_DEVICE;
   rc_stream_state rel = *state;
-  rel.pos -= p0;  // the window starts at p0 (stage 0: at the stream start, pos is unused)
+  rel.pos -= p0;  // the window starts at p0 (stage 0: at the stream start)
+  memcpy(h, &rel, sizeof rel);
   const u64 offs[4] = {0, wlen, 0, n};
-  bool ok = hipMemcpyAsync(d, &rel, sizeof rel, hipMemcpyHostToDevice, s) == hipSuccess &&
-            hipMemcpyAsync(d + o_off, offs, sizeof offs, hipMemcpyHostToDevice, s) == hipSuccess &&
-            hipMemcpyAsync(d + o_c, c, 4ull * n_symbols, hipMemcpyHostToDevice, s) == hipSuccess &&
-            hipMemcpyAsync(d + o_cum, cum, 4ull * n_symbols, hipMemcpyHostToDevice, s) ==
-                hipSuccess &&
-            (!wlen || hipMemcpyAsync(d + o_win, code + p0, wlen, hipMemcpyHostToDevice, s) ==
-                          hipSuccess);
-  if (!ok) return RC_E_DEVICE;
+  memcpy(h + o_off, offs, sizeof offs);
+  memcpy(h + o_c, c, 4ull * n_symbols);
+  memcpy(h + o_cum, cum, 4ull * n_symbols);
+  if (wlen) memcpy(h + o_win, code + p0, wlen);
+  if (hipMemcpyAsync(d, h, o_win + wlen, hipMemcpyHostToDevice, s) != hipSuccess)
+    return RC_E_DEVICE;
   hipLaunchKernelGGL(k_stream_decode, dim3(1), dim3(RWG), 0, s, (const u32*)(d + o_c),
                      (const u32*)(d + o_cum), n_symbols, total_freq, (rc_stream_state*)d,
                      (const uint8_t*)(d + o_win), (const u64*)(d + o_off),
                      (const u64*)(d + o_off + 8), (uint8_t*)(d + o_sym),
                      (const u64*)(d + o_off + 16), 1u, (u32*)(d + o_fl));
   if (hipGetLastError() != hipSuccess) return RC_E_DEVICE;
-  rc_stream_state nst;
-  u32 fl = 0;
-  ok = hipMemcpyAsync(&nst, d, sizeof nst, hipMemcpyDeviceToHost, s) == hipSuccess &&
-       hipMemcpyAsync(&fl, d + o_fl, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-       hipStreamSynchronize(s) == hipSuccess;
-  if (!ok) return RC_E_DEVICE;
-  const u64 got = nst.n - state->n;
-  if (got && hipMemcpyAsync(syms, d + o_sym, got, hipMemcpyDeviceToHost, s) != hipSuccess)
+  if (hipMemcpyAsync(h, d, o_c, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      (n && hipMemcpyAsync(h + o_sym, d + o_sym, n, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+      hipStreamSynchronize(s) != hipSuccess)
     return RC_E_DEVICE;
-  if (hipStreamSynchronize(s) != hipSuccess) return RC_E_DEVICE;
+  rc_stream_state nst;
+  u32 fl;
+  memcpy(&nst, h, sizeof nst);
+  memcpy(&fl, h + o_fl, 4);
+  const u64 got = nst.n - state->n;
+  if (got > n) return RC_E_DEVICE;
+  if (got) memcpy(syms, h + o_sym, got);
   nst.pos += p0;
   *state = nst;
   if (flags_out) *flags_out = fl;
   return fl ? RC_E_CHUNK : RC_OK;
+}
+
+// internal: free the context's staging block (called by rc_ctx_destroy)
+void rc_resume_release_(const rc_ctx* ctx) {
+  Stage st;
+  {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    auto it = g_stages.find(ctx);
+    if (it == g_stages.end()) return;
+    st = it->second;
+    g_stages.erase(it);
+  }
+  if (st.host) (void)hipHostFree(st.host);
+  if (st.dev) (void)hipFree(st.dev);
 }
 
 }  // extern "C"

@@ -14,7 +14,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -43,18 +45,22 @@ struct DevSet {
   }
 };
 
+// set on the worker threads of rc_*_multi, which page-locked the caller's whole buffers once:
+// a worker registering a sub-range again would, on unregistering it, unpin the whole range
+thread_local bool t_pinned_by_caller = false;
+
 // page-lock a caller buffer for the duration of the call (no-op if it is already pinned)
 struct Pin {
   void* p = nullptr;
   bool mine = false;
-  Pin(const void* ptr, size_t n) {
-    if (!ptr || !n) return;
+  Pin(const void* ptr, size_t n, unsigned flags = hipHostRegisterDefault) {
+    if (!ptr || !n || t_pinned_by_caller) return;
     p = const_cast<void*>(ptr);
-    mine = hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess;
+    mine = hipHostRegister(p, n, flags) == hipSuccess;
     if (!mine) (void)hipGetLastError();  // already registered / pinned: fine either way
   }
   ~Pin() {
-    if (mine) (void)hipHostUnregister(p);
+    if (mine && hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
   }
 };
 
@@ -362,6 +368,93 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   if (!p.drain()) return RC_E_DEVICE;
   memcpy(flags, p.hfl, 4ull * n_chunks);
   return any_flag(flags, n_chunks);
+}
+
+}  // extern "C"
+
+// ---- several devices from one host thread (rc_*_multi) ----
+namespace {
+
+// contiguous chunk ranges of about equal input bytes, one per context
+std::vector<u32> split_by_bytes(u32 n, u32 parts, const std::function<u64(u32)>& bytes_of) {
+  std::vector<u64> pre(n + 1, 0);
+  for (u32 k = 0; k < n; ++k) pre[k + 1] = pre[k] + bytes_of(k);
+  std::vector<u32> cut(parts + 1, n);
+  cut[0] = 0;
+  for (u32 i = 1; i < parts; ++i) {
+    const u64 target = pre[n] / parts * i + std::min<u64>(pre[n] % parts, i);
+    cut[i] = (u32)(std::lower_bound(pre.begin(), pre.end(), target) - pre.begin());
+    cut[i] = std::max(cut[i], cut[i - 1]);
+  }
+  return cut;
+}
+
+template <class F>
+rc_status run_parts(u32 n_ctx, const std::vector<u32>& cut, F f) {
+  std::vector<rc_status> st(n_ctx, RC_OK);
+  std::vector<std::thread> th;
+  for (u32 i = 0; i < n_ctx; ++i)
+    if (cut[i + 1] > cut[i])
+      th.emplace_back([&, i] {
+        t_pinned_by_caller = true;  // the multi call holds the pins
+        st[i] = f(i, cut[i], cut[i + 1] - cut[i]);
+      });
+  for (auto& t : th) t.join();
+  rc_status res = RC_OK;
+  for (rc_status x : st)
+    if (x != RC_OK && (res == RC_OK || res == RC_E_CHUNK)) res = x;
+  return res;
+}
+
+}  // namespace
+
+extern "C" {
+
+rc_status rc_encode_host_multi(rc_ctx* const* ctxs, const rc_model* const* models, uint32_t n_ctx,
+                               const uint8_t* syms, const uint64_t* sym_off, uint32_t n_chunks,
+                               uint8_t* out, const uint64_t* out_off, uint64_t* out_len,
+                               uint32_t* flags) {
+  if (!ctxs || !models || n_ctx == 0 || n_chunks > RC_MAX_CHUNKS) return RC_E_ARG;
+  if (n_chunks == 0) return RC_OK;
+  if (!syms || !sym_off || !out || !out_off || !out_len || !flags) return RC_E_ARG;
+  for (u32 i = 0; i < n_ctx; ++i)
+    if (!ctxs[i] || !models[i]) return RC_E_ARG;
+  for (u32 k = 0; k < n_chunks; ++k)
+    if (sym_off[k + 1] < sym_off[k] || out_off[k + 1] < out_off[k]) return RC_E_ARG;
+  // pinned once for every device (each device's call then finds its range already pinned)
+  Pin pin_in(syms + sym_off[0], sym_off[n_chunks] - sym_off[0], hipHostRegisterPortable);
+  Pin pin_out(out + out_off[0], out_off[n_chunks] - out_off[0], hipHostRegisterPortable);
+  const std::vector<u32> cut =
+      split_by_bytes(n_chunks, n_ctx, [&](u32 k) { return sym_off[k + 1] - sym_off[k]; });
+  return run_parts(n_ctx, cut, [&](u32 i, u32 k0, u32 nk) {
+    return rc_encode_host(ctxs[i], models[i], syms, sym_off + k0, nk, out, out_off + k0,
+                          out_len + k0, flags + k0);
+  });
+}
+
+rc_status rc_decode_host_multi(rc_ctx* const* ctxs, const rc_model* const* models, uint32_t n_ctx,
+                               const uint8_t* code, const uint64_t* code_off,
+                               const uint64_t* code_len, uint8_t* syms_out,
+                               const uint64_t* sym_off, uint32_t n_chunks, uint32_t* flags) {
+  if (!ctxs || !models || n_ctx == 0 || n_chunks > RC_MAX_CHUNKS) return RC_E_ARG;
+  if (n_chunks == 0) return RC_OK;
+  if (!code || !code_off || !code_len || !syms_out || !sym_off || !flags) return RC_E_ARG;
+  for (u32 i = 0; i < n_ctx; ++i)
+    if (!ctxs[i] || !models[i]) return RC_E_ARG;
+  for (u32 k = 0; k < n_chunks; ++k)
+    if (sym_off[k + 1] < sym_off[k]) return RC_E_ARG;
+  u64 cmin = ~0ull, cmax = 0;
+  for (u32 k = 0; k < n_chunks; ++k) {
+    cmin = std::min(cmin, code_off[k]);
+    cmax = std::max(cmax, code_off[k] + code_len[k]);
+  }
+  Pin pin_in(code + cmin, cmax - cmin, hipHostRegisterPortable);
+  Pin pin_out(syms_out + sym_off[0], sym_off[n_chunks] - sym_off[0], hipHostRegisterPortable);
+  const std::vector<u32> cut = split_by_bytes(n_chunks, n_ctx, [&](u32 k) { return code_len[k]; });
+  return run_parts(n_ctx, cut, [&](u32 i, u32 k0, u32 nk) {
+    return rc_decode_host(ctxs[i], models[i], code, code_off + k0, code_len + k0, syms_out,
+                          sym_off + k0, nk, flags + k0);
+  });
 }
 
 // internal: free the context's cached pipeline (called by rc_ctx_destroy)

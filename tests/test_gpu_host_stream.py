@@ -133,3 +133,29 @@ def test_cached_pipeline_across_shapes(monkeypatch):
         del m
     finally:
         own.close()
+
+
+def test_host_multi_device_list_equals_single(ctx):
+    """rc_encode_host_multi / rc_decode_host_multi over a list of contexts — here two contexts
+    on the one visible device (each with its own streams and pipeline) plus the default one:
+    the chunks split three ways give the bytes of one single-device call."""
+    c, cum, total = synth.zipf_table()
+    inv = synth.inverse_cdf(c)
+    n, L = 300, 3000
+    syms = np.concatenate([synth.host_chunk(0x77, inv, k, L + (k % 7) * 13) for k in range(n)])
+    lens = np.array([L + (k % 7) * 13 for k in range(n)], np.uint64)
+    soff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    caps = np.array([rc.slot_capacity(int(x), 8.0) for x in lens], np.uint64)
+    ooff = np.concatenate([[0], np.cumsum(caps)]).astype(np.uint64)
+    ctxs = [rc.default_context(0), rc.Context(0), rc.Context(0)]
+    models = [rc.StaticModel(c, cum, total, ctx=x) for x in ctxs]
+    out1, ol1, fl1 = rc.encode_host(models[0], syms, soff, ooff)
+    out3, ol3, fl3 = rc.encode_host_multi(models, syms, soff, ooff)
+    assert (fl1 == 0).all() and (fl3 == 0).all() and np.array_equal(ol1, ol3)
+    for k in range(n):
+        assert out1[ooff[k]: ooff[k] + ol1[k]].tobytes() == out3[ooff[k]: ooff[k] + ol3[k]].tobytes()
+    dec, fd = rc.decode_host_multi(models, out3, ooff[:-1], ol3, soff)
+    assert (fd == 0).all() and np.array_equal(dec, syms)
+    for k in (0, n // 2, n - 1):
+        f, b, lb = cpu.encode(c, cum, total, syms[soff[k]: soff[k + 1]])
+        assert f == 0 and out3[ooff[k]: ooff[k] + lb].tobytes() == b

@@ -303,3 +303,31 @@ def test_stream_positions_are_64_bit(ctx):
     assert int(fl[0]) == 0
     assert np.array_equal(out.cpu().numpy(), syms[100:])
     assert int(states.cpu().numpy().view(np.uint64)[0, 3]) == big + len(code)
+
+
+def _xorshift_syms(n, seed):
+    """The symbol generator of examples/adaptive_impl.cpp."""
+    x, out, M = seed, [], (1 << 64) - 1
+    for _ in range(n):
+        x ^= (x << 13) & M
+        x ^= x >> 7
+        x ^= (x << 17) & M
+        r = x % 1000
+        out.append(r % 4 if r < 500 else (r % 32 if r < 800 else r % 256))
+    return out
+
+
+def test_cpp_caller_adaptive_model(ctx):
+    """examples/adaptive_impl.cpp: rc::Encoder / rc::Decoder with a PModel the caller updates
+    between calls; its stream equals the literal restatement's."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples",
+                       "adaptive_impl")
+    if not os.path.exists(exe):
+        pytest.skip("examples/adaptive_impl not built")
+    n, seed = 3000, 5
+    r = subprocess.run([exe, str(n), str(seed)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    want = R.encode_adaptive_stream(256, 32, 4000, 64, _xorshift_syms(n, seed))
+    assert r.stdout.strip() == want.hex()
