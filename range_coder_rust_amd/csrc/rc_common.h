@@ -30,11 +30,15 @@ typedef u32 u32x3 __attribute__((ext_vector_type(3)));
 static __device__ __forceinline__ u32 hi32(u64 v) { return (u32)(v >> 32); }
 
 // a - b (64-bit) with the borrow in an SGPR pair: the compiler's v_subb_co_u32_e32 reads VCC,
-// and a VALU read of VCC costs ~13 extra SIMD cycles on gfx950 (tools/ubench_issue.hip)
+// and a VALU read of VCC costs ~13 extra SIMD cycles on gfx950 (tools/ubench_issue.hip).
+// A VALU write of an SGPR read by a VALU as its carry-in needs 2 wait states on gfx950 (hipcc
+// pads its own v_sub_co -> v_subb_co_e64 pairs with them; it pads nothing inside an asm
+// string): the s_nop 1 between the two.  Without it the borrow may be read stale
+// (DESIGN.md §6).
 static __device__ __forceinline__ u64 sub64(u64 a, u64 b) {
   u32 lo, hi;
   u64 c;
-  asm("v_sub_co_u32_e64 %0, %2, %3, %4\n\tv_subb_co_u32_e64 %1, %2, %5, %6, %2"
+  asm("v_sub_co_u32_e64 %0, %2, %3, %4\n\ts_nop 1\n\tv_subb_co_u32_e64 %1, %2, %5, %6, %2"
       : "=&v"(lo), "=&v"(hi), "=&s"(c)
       : "v"((u32)a), "v"((u32)b), "v"(hi32(a)), "v"(hi32(b)));
   return ((u64)hi << 32) | lo;
@@ -43,7 +47,7 @@ static __device__ __forceinline__ u64 sub64(u64 a, u64 b) {
 static __device__ __forceinline__ u64 sub64(u32 alo, u32 ahi, u64 b) {
   u32 lo, hi;
   u64 c;
-  asm("v_sub_co_u32_e64 %0, %2, %3, %4\n\tv_subb_co_u32_e64 %1, %2, %5, %6, %2"
+  asm("v_sub_co_u32_e64 %0, %2, %3, %4\n\ts_nop 1\n\tv_subb_co_u32_e64 %1, %2, %5, %6, %2"
       : "=&v"(lo), "=&v"(hi), "=&s"(c)
       : "v"(alo), "v"((u32)b), "v"(ahi), "v"(hi32(b)));
   return ((u64)hi << 32) | lo;
