@@ -44,8 +44,9 @@ typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 static __device__ __forceinline__ u32 clz32(u32 v) { return (u32)__builtin_clz(v); }  // v != 0
 
 // ~1/t to well under 2^-40 relative error: v_rcp_f64 plus one Newton step
+static __device__ __forceinline__ double cvt_f64(u32 v);
 static __device__ __forceinline__ double recip(u32 t) {
-  const double d = (double)t;
+  const double d = cvt_f64(t);
   const double r = __builtin_amdgcn_rcp(d);
   return fma(r, fma(-d, r, 1.0), r);
 }
@@ -56,24 +57,53 @@ static __device__ __forceinline__ double recip(u32 t) {
 // v_addc_co_u32) costs ~4x a plain op on gfx950 (tools/ubench_sel.hip).
 static __device__ __forceinline__ u32 fixup(u32& q, u32 rem, u32 t) {  // rem < 2t
   const u32 d = rem - t;
-  q += 1u + (u32)((int)d >> 31);  // +1 unless rem < t
-  return min(rem, d);             // rem mod t
+  // q + 1 + (d >> 31 arithmetic): +1 unless rem < t, one v_add3_u32 (the compiler's form of
+  // it is a not, a shift and an add)
+  asm("v_add3_u32 %0, %0, 1, %1" : "+v"(q) : "v"((u32)((int)d >> 31)));
+  return min(rem, d);  // rem mod t
 }
 static __device__ __forceinline__ u64 div_total(u64 v, u32 t, double rt) {
   const u32 hi = hi32(v), lo = (u32)v;
-  u32 qh = (u32)((double)hi * rt);
+  u32 qh = (u32)(cvt_f64(hi) * rt);
   const u32 rh = fixup(qh, hi - qh * t, t);
-  const double num = fma((double)rh, 4294967296.0, (double)lo);  // < 2^48: exact
+  const double num = fma(cvt_f64(rh), 4294967296.0, cvt_f64(lo));  // < 2^48: exact
   u32 ql = (u32)(num * rt);
   fixup(ql, lo - ql * t, t);  // (rh:lo) - ql*t < 2t: its low 32 bits are the value
   return ((u64)qh << 32) | ql;
 }
 
+// range_par_total (range_coder.rs:38-40): floor(v / t) for 1 <= t < 2^16 from the model's
+// table entry M = floor((2^64 - 1) / t): q = mulhi(v, M) is floor(v / t) or one less (v < 2^64,
+// so v / 2^64 < 1 is all M's truncation can lose), and v - q t < 2t tells which, in 32 bits.
+static __device__ __forceinline__ u64 div_magic(u64 v, u32 t, u64 M) {
+  u64 q = __umul64hi(v, M);
+  const u32 rem = (u32)v - (u32)q * t;  // < 2t: its low 32 bits are the remainder
+  return q + (1u + (u32)((int)(rem - t) >> 31));
+}
+
 // (m & a) | (~m & b) for a mask m of 0 / ~0: one v_bfi_b32.  The empty asm hides that m is a
 // mask, or the compiler turns this back into v_cmp + v_cndmask_b32 on VCC.
 static __device__ __forceinline__ u32 msel(u32 m, u32 a, u32 b) {
-  asm("" : "+v"(m));
-  return (m & a) | (~m & b);
+  u32 r;  // written out: from the C form the compiler narrows selects of u16 tree values to
+          // 16-bit xor / and / bitop3 sequences and re-extends their results
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+
+// the sign of v as a mask (0 / ~0), opaque to the compiler (which otherwise turns selects on it
+// back into v_cmp + v_cndmask_b32 on VCC)
+static __device__ __forceinline__ u32 smask(u32 v) {
+  u32 r;
+  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// u32 -> f64 as the single instruction (the compiler widens (double)hi32(x) into a u64
+// conversion: a second convert and an f64 add)
+static __device__ __forceinline__ double cvt_f64(u32 v) {
+  double d;
+  asm("v_cvt_f64_u32 %0, %1" : "=v"(d) : "v"(v));
+  return d;
 }
 
 // r * v for v < 2^16 (r < 2^64 / v: no overflow)
@@ -562,54 +592,17 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // ------------------------------------------------------------------------------------------
 // Decoder
 // ------------------------------------------------------------------------------------------
-
-// The code of one lane: r[0..fill) are stream dwords (memory order), the read position at
-// byte off of r[0]; pend is the 16-B block after them, loaded one phase ahead.
-struct Win {
-  u32 r[8];
-  u32 off, fill;
-  u32x4 pend;
-  const u32x4* pnx;    // address of pend
-  const u32x4* plast;  // last 16-B block holding a code byte
-};
-
-// the 4 code bytes at the read position, big-endian (needs fill >= 2)
-static __device__ __forceinline__ u32 win_peek(const Win& w) {
-  return __builtin_bswap32(__builtin_amdgcn_alignbyte(w.r[1], w.r[0], w.off));
-}
-
-// consume kb <= 3 bytes (Decoder::shift_left_buffer, decoder.rs:31-35)
-static __device__ __forceinline__ void win_adv(Win& w, u32 kb) {
-  const u32 o = w.off + kb;
-  const u32 sh = o >> 2;  // 0 or 1: a whole dword consumed
-  const u32 m = 0u - sh;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) w.r[i] = msel(m, w.r[i + 1], w.r[i]);
-  w.off = o & 3u;
-  w.fill -= sh;
-}
-
-// r[fill .. fill + 4) = pend (fill <= 4), and advance to the next block: pend shifted up by
-// fill slots (a 3-stage barrel on fill's bits), merged above the valid dwords
-static __device__ __forceinline__ void win_append(Win& w) {
-  const u32 f = w.fill;
-  const u32 m1 = 0u - (f & 1u), m2 = 0u - ((f >> 1) & 1u), m4 = 0u - ((f >> 2) & 1u);
-  const u32 p[4] = {w.pend.x, w.pend.y, w.pend.z, w.pend.w};
-  u32 a[5], b[7], c[8];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) a[i] = msel(m1, i >= 1 ? p[i - 1] : 0u, i < 4 ? p[i] : 0u);
-#pragma unroll
-  for (int i = 0; i < 7; ++i) b[i] = msel(m2, i >= 2 ? a[i - 2] : 0u, i < 5 ? a[i] : 0u);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) c[i] = msel(m4, i >= 4 ? b[i - 4] : 0u, i < 7 ? b[i] : 0u);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const u32 keep = (u32)((int)((u32)i - f) >> 31);  // i < fill
-    w.r[i] = msel(keep, w.r[i], c[i]);
-  }
-  w.fill += 4;
-  w.pnx = w.pnx < w.plast ? w.pnx + 1 : w.plast;
-}
+//
+// The decoder is bound by how fast ONE wave issues: the 32 KiB tree per wave leaves room for 5
+// waves per CU, so most SIMDs run a single wave, which issues an instruction every ~4-5 cycles
+// whatever the instruction (profiles/r02/pmc_adaptive_*.txt: 73% of wave time issuing, 23%
+// waiting).  The symbol step is therefore written for instruction count:
+//  * the code window is three dwords in registers, (cpos & ~3) + 0, 4, 8, shifted by one dword
+//    when a symbol crosses a dword boundary; the next dword is loaded then, by the crossing
+//    lanes only, and is needed no earlier than the next crossing (one symbol later at least);
+//  * the walk tracks ~rem and (upper bound - q - 1), so each level is one add, one sign mask,
+//    one max, one min and the path bit; the count comes out as e1 - ~rem;
+//  * r * cum and r * c for 256-symbol models are a 64-bit mad plus a 24-bit mad each.
 
 // u32 -> f32 and f32 -> u32 (saturating) as single instructions
 static __device__ __forceinline__ float cvt_f32(u32 v) {
@@ -623,159 +616,204 @@ static __device__ __forceinline__ u32 cvt_u32_sat(float f) {
   return v;
 }
 
+// r * v (range_coder.rs:65, :70).  SM (256-symbol models, so total >= 256): r < 2^56 and
+// v < 2^16, so the high half is a 24-bit mad into the high half of lo(r) * v.
+template <int SM>
+static __device__ __forceinline__ u64 mul_rs(u64 r, u32 v) {
+  if (SM) {
+    u64 p, c;
+    u32 h;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(c) : "v"((u32)r), "v"(v));
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(r)), "v"(v), "v"(hi32(p)));
+    return ((u64)h << 32) | (u32)p;
+  }
+  return mul_r(r, v);
+}
+
+// the code of one chunk: its dword-aligned origin and the offset of the last dword holding a
+// code byte (every load is clamped to it, so none leaves the chunk's last dword)
+struct ACode {
+  const uint8_t* o;
+  u32 dwl;
+};
+static __device__ __forceinline__ u32 ldw(const ACode& g, u32 off) {
+  return gload((const u32*)(g.o + off));
+}
+
 struct ADec {
-  u64 low, range, x;  // x = Decoder::data - lower_bound (mod 2^64): all find_index needs
-  u32 total, used;    // used: code bytes consumed (8 primed + shifted in)
-  float tf;           // (float)total
-  double rt;          // ~1 / total
-  u32 L0, L1a, L1b, L2a, L2b, L2c, L2d;  // tree levels 0-2 (fixed nodes), read one symbol ahead
+  u64 low, range;
+  u32 xlo, xhi;  // x = Decoder::data - lower_bound (mod 2^64): all find_index needs
+  u32 total;
+  float tf;      // (float)total
+  u64 M, Mn;     // magic[total] for this symbol, magic[total + inc] (loaded one symbol ahead)
+  u32 cpos;      // origin-relative position of the next code byte (a + 8 primed + shifted in)
+  u32 D0, D1, D2;  // the code dwords at (cpos & ~3) + 0, 4, 8 (offsets clamped to dwl)
+  u32 d2o;         // offset of D2
+  u32 L0, L1a, L1b, L2a, L2b, L2c, L2d;  // tree levels 0-2 (fixed nodes) of this symbol
 };
 
-static __device__ __forceinline__ void dec_preread(ADec& d, l_char* tb, u32 col) {
-  d.L0 = LRD(tb, col + ROW(128));
-  d.L1a = LRD(tb, col + ROW(64));
-  d.L1b = LRD(tb, col + ROW(192));
-  d.L2a = LRD(tb, col + ROW(32));
-  d.L2b = LRD(tb, col + ROW(96));
-  d.L2c = LRD(tb, col + ROW(160));
-  d.L2d = LRD(tb, col + ROW(224));
+static __device__ __forceinline__ void dec_preread(ADec& d, u32 col) {
+  d.L0 = lrd(col + ROW(128));
+  d.L1a = lrd(col + ROW(64));
+  d.L1b = lrd(col + ROW(192));
+  d.L2a = lrd(col + ROW(32));
+  d.L2b = lrd(col + ROW(96));
+  d.L2c = lrd(col + ROW(160));
+  d.L2d = lrd(col + ROW(224));
+}
+
+// nb <= 3 code bytes consumed (Decoder::shift_left_buffer, decoder.rs:31-35): a whole dword is
+// consumed when bit 2 of the position flips.  Every lane then (re)loads the dword after its
+// window (the same one when it did not cross): a load into the loop-carried register only for
+// the crossing lanes makes the compiler copy that register, and wait for the load to do it.
+static __device__ __forceinline__ void win_step(ADec& d, const ACode& g, u32 nb) {
+  const u32 c2 = d.cpos + nb;
+  const u32 mc = smask((d.cpos ^ c2) << 29);  // ~0: crossed into the next dword
+  d.D0 = msel(mc, d.D1, d.D0);
+  d.D1 = msel(mc, d.D2, d.D1);
+  d.d2o = min(d.d2o + (mc & 4u), g.dwl);
+  d.D2 = ldw(g, d.d2o);
+  d.cpos = c2;
 }
 
 // The walk for target q < total: symbol s, cum[s], c[s], and per level the visited node's
-// row base P[l] (its node at P[l] + ROW(128 >> l)) and updated value nv[l] (+inc on a left turn)
+// row base P[l] (its node at P[l] + ROW(128 >> l)) and updated value nv[l] (+inc on a left
+// turn).  It tracks nrem = ~rem and e1 = (upper end of the current subtree) - q - 1: with
+// nd = v + nrem = ~(rem - v), a right turn (rem >= v) is nd < 0, rem' = min(rem, rem - v) is
+// nrem' = max(nrem, nd), and a left turn makes the upper end cum + v, so e1' = min(e1, nd)
+// (a right turn leaves it: nd is then >= 2^32 - 2^16 > e1).  At the end c = e1 + 1 + rem =
+// e1 - nrem.
 struct DWalk {
   u32 s, cum, c;
   u32 nv[8], P[8];
 };
 
-static __device__ __forceinline__ void dec_walk(DWalk& w, const ADec& d, l_char* tb, u32 q,
-                                                u32 col, u32 inc) {
-  u32 rem = q, b = d.total, P = col;
-  u32 m[8];  // ~0: the walk turned left at that level (rem < node)
-#define RC_LEVEL(l, V)                                   \
-  {                                                      \
-    const u32 v_ = (V), d_ = rem - v_;                   \
-    m[l] = (u32)((int)d_ >> 31);                         \
-    w.nv[l] = v_ + (inc & m[l]);                         \
-    w.P[l] = P;                                          \
-    rem = min(rem, d_);                                  \
-    b = msel(m[l], v_, b - v_);                          \
-    P |= ~m[l] & ((128u >> (l)) * 128u);                 \
+static __device__ __forceinline__ void dec_walk(DWalk& w, const ADec& d, u32 q, u32 col,
+                                                u32 inc) {
+  u32 nrem = ~q, e1 = d.total + nrem, P = col;
+  u32 mr[8];  // ~0: the walk turned right at that level
+#define RC_LEVEL(l, V)                                  \
+  {                                                     \
+    const u32 v_ = (V), nd_ = v_ + nrem;                \
+    mr[l] = smask(nd_);                                 \
+    w.nv[l] = v_ + msel(mr[l], 0u, inc);                \
+    w.P[l] = P;                                         \
+    nrem = max(nrem, nd_);                              \
+    e1 = min(e1, nd_);                                  \
+    P |= mr[l] & ((128u >> (l)) * 128u);                \
   }
   RC_LEVEL(0, d.L0)
-  RC_LEVEL(1, msel(m[0], d.L1a, d.L1b))
+  RC_LEVEL(1, msel(mr[0], d.L1b, d.L1a))
   {
-    const u32 t0 = msel(m[0], d.L2a, d.L2c), t1 = msel(m[0], d.L2b, d.L2d);
-    RC_LEVEL(2, msel(m[1], t0, t1))
+    const u32 t0 = msel(mr[0], d.L2c, d.L2a), t1 = msel(mr[0], d.L2d, d.L2b);
+    RC_LEVEL(2, msel(mr[1], t1, t0))
   }
   {  // levels 3-5: one 7-node read below P
-    const u32 r3 = LRD(tb, P + ROW(16)), r4a = LRD(tb, P + ROW(8)), r4b = LRD(tb, P + ROW(24));
-    const u32 r5a = LRD(tb, P + ROW(4)), r5b = LRD(tb, P + ROW(12));
-    const u32 r5c = LRD(tb, P + ROW(20)), r5d = LRD(tb, P + ROW(28));
+    const u32 r3 = lrd(P + ROW(16)), r4a = lrd(P + ROW(8)), r4b = lrd(P + ROW(24));
+    const u32 r5a = lrd(P + ROW(4)), r5b = lrd(P + ROW(12));
+    const u32 r5c = lrd(P + ROW(20)), r5d = lrd(P + ROW(28));
     RC_LEVEL(3, r3)
-    RC_LEVEL(4, msel(m[3], r4a, r4b))
-    const u32 u0 = msel(m[3], r5a, r5c), u1 = msel(m[3], r5b, r5d);
-    RC_LEVEL(5, msel(m[4], u0, u1))
+    RC_LEVEL(4, msel(mr[3], r4b, r4a))
+    const u32 u0 = msel(mr[3], r5c, r5a), u1 = msel(mr[3], r5d, r5b);
+    RC_LEVEL(5, msel(mr[4], u1, u0))
   }
   {  // levels 6-7: one 3-node read
-    const u32 r6 = LRD(tb, P + ROW(2)), r7a = LRD(tb, P + ROW(1)), r7b = LRD(tb, P + ROW(3));
+    const u32 r6 = lrd(P + ROW(2)), r7a = lrd(P + ROW(1)), r7b = lrd(P + ROW(3));
     RC_LEVEL(6, r6)
-    RC_LEVEL(7, msel(m[6], r7a, r7b))
+    RC_LEVEL(7, msel(mr[6], r7b, r7a))
   }
 #undef RC_LEVEL
   w.s = (P - col) >> 7;
-  w.cum = q - rem;
-  w.c = b;
+  w.cum = q + nrem + 1u;  // q - rem
+  w.c = e1 - nrem;
 }
 
 // c[s] += inc on the walked path
-static __device__ __forceinline__ void dec_update(const DWalk& w, l_char* tb) {
+static __device__ __forceinline__ void dec_update(const DWalk& w) {
 #pragma unroll
-  for (int l = 0; l < 8; ++l) LWR(tb, w.P[l] + ROW(128u >> l), w.nv[l]);
+  for (int l = 0; l < 8; ++l) lwr(w.P[l] + ROW(128u >> l), w.nv[l]);
 }
 
 // Decoder::decode (decoder.rs:38-54) with FreqTable::find_index (sample_impl.rs:27-45) and the
 // model update; returns the symbol.  Wave-uniform call sites only (rare branches inside).
-// the period's halving check after symbol i (adapt_update)
-static __device__ __forceinline__ void dec_halve(ADec& d, l_char* tb, uint16_t* tcol, u32 col) {
-  tree_halve(tcol, d.total);
-}
-
-// at: symbol i is a period end ((i + 1) % period == 0); uni: at is wave-uniform
-template <bool UNI>
-static __device__ __forceinline__ u32 dec_step(ADec& d, Win& w, l_char* tb, u32 col,
-                                               uint16_t* tcol, const AdaptParams& p, bool at) {
-  if (__builtin_expect(__any((int)(w.fill < 2)), 0)) {  // the window ran short (rare)
-    if (w.fill < 2) {
-      win_append(w);
-      w.pend = gload16(w.pnx);
-    }
-  }
-  const u32 nb4 = win_peek(w);
-  // hint q ~ x * total / range from the high halves (range >= 2^48: relative error <= 2^-15)
-  const float X = cvt_f32(hi32(d.x)), R = cvt_f32(hi32(d.range));
-  const u32 q = min(cvt_u32_sat(X * (d.tf * __builtin_amdgcn_rcpf(R))), d.total - 1);
-  const u64 r = div_total(d.range, d.total, d.rt);
+// at: symbol i is a period end ((i + 1) % period == 0); UNI: at is wave-uniform.
+template <bool UNI, int SM>
+static __device__ __forceinline__ u32 dec_step(ADec& d, const ACode& g, u32 col, uint16_t* tcol,
+                                               const AdaptParams& p, bool at) {
+  // levels 0-2 of the tree (fixed nodes) first: their LDS latency hides behind the hint and
+  // range / total.  (Read at the end of the previous symbol and carried instead, they are
+  // re-zero-extended by the compiler at the loop latch, which also waits for them there.)
+  dec_preread(d, col);
+  // hint q ~ x * total / range from the high halves (range >= 2^48: relative error <= 2^-15),
+  // clamped to total - 1: the walk's upper-end tracking relies on q < total
+  const float X = cvt_f32(d.xhi), R = cvt_f32(hi32(d.range));
+  const u32 q = min(cvt_u32_sat(X * (d.tf * __builtin_amdgcn_rcpf(R))), d.total - 1u);
+  const u64 r = div_magic(d.range, d.total, d.M);
   DWalk wk;
-  dec_walk(wk, d, tb, q, col, p.inc);
-  u64 A = mul_r(r, wk.cum), B = mul_r(r, wk.c);
-  u64 dx = sub64(d.x, A);
+  dec_walk(wk, d, q, col, p.inc);
+  u64 A = mul_rs<SM>(r, wk.cum), B = mul_rs<SM>(r, wk.c);
+  u64 dx = sub64(d.xlo, d.xhi, A);
   // exact check r*cum <= x < r*(cum+c) as one unsigned test (A + B <= range: a wrapped x - A
   // is >= B)
   if (__builtin_expect(__any((int)(dx >= B)), 0)) {
     if (dx >= B) {  // exact rfreq = min(x / r, total - 1), then the walk again
+      const u64 x = ((u64)d.xhi << 32) | d.xlo;
       u32 qe = d.total - 1;
-      if (d.x < mul_r(r, d.total)) {
-        qe = q;
+      if (x < mul_r(r, d.total)) {
+        qe = min(q, d.total - 1);
         u64 a = mul_r(r, qe);
-        while (a > d.x) {
+        while (a > x) {
           --qe;
           a -= r;
         }
-        while (d.x - a >= r) {
+        while (x - a >= r) {
           ++qe;
           a += r;
         }
       }
-      dec_walk(wk, d, tb, qe, col, p.inc);
+      dec_walk(wk, d, qe, col, p.inc);
       A = mul_r(r, wk.cum);
       B = mul_r(r, wk.c);
-      dx = sub64(d.x, A);
+      dx = sub64(d.xlo, d.xhi, A);
     }
   }
-  dec_update(wk, tb);
+  dec_update(wk);
   d.total += p.inc;
+  d.M = d.Mn;  // magic[total], loaded during this symbol unless a halving changes the total
   if (!UNI || at) {  // the halving check, before the next symbol's tree reads
     const bool h = at && d.total > p.limit;
     if (__builtin_expect(__any((int)h), 0)) {
-      if (h) tree_halve(tcol, d.total);
+      if (h) {
+        tree_halve(tcol, d.total);
+        d.M = gload64(p.magic + d.total);
+      }
     }
   }
-  dec_preread(d, tb, col);
+  d.Mn = gload64(p.magic + (d.total + p.inc));  // for the next symbol (total < 2^16 - inc)
   d.tf = (float)d.total;
-  d.rt = recip(d.total);
   // param_update (range_coder.rs:53-92), closed form (<= 3 bytes: range >= 2^32 here)
   d.low += A;
-  d.range = B;
-  const u32 k8 = clz32(hi32(d.low) ^ hi32(d.low + d.range)) & 24u;
+  const u32 k8 = clz32(hi32(d.low) ^ hi32(d.low + B)) & 24u;
   d.low <<= k8;
-  d.range <<= k8;
-  // data' = data << k8 | bytes and low' = (low + A) << k8: x' = (x - A) << k8 | bytes
-  d.x = ((u64)hi32(dx << k8) << 32) | hi32((((u64)(u32)dx) << 32 | nb4) << k8);
-  win_adv(w, k8 >> 3);
-  d.used += k8 >> 3;
+  d.range = B << k8;
+  // data' = data << k8 | bytes and low' = (low + A) << k8, so x' = (x - A) << k8 | the k8 / 8
+  // code bytes at cpos: xl is ONE v_perm_b32 over {dx_lo, W} with selector
+  // hi32(0x0706050400010203 << k8) (W = the 4 code bytes at cpos, first byte in byte 0)
+  const u32 W = __builtin_amdgcn_alignbyte(d.D1, d.D0, d.cpos);
+  d.xlo = __builtin_amdgcn_perm((u32)dx, W, hi32(0x0706050400010203ull << k8));
+  d.xhi = hi32(dx << k8);
+  u32 nb;  // k8 >> 3 as a plain shift (the compiler's v_bfe from the clz result costs more)
+  asm("v_lshrrev_b32 %0, 3, %1" : "=v"(nb) : "v"(k8));
+  win_step(d, g, nb);
   if (__builtin_expect(__any((int)(hi32(d.range) < 0x10000u)), 0)) {
     while (d.range < TOP16) {  // range_reduction_expansion (range_coder.rs:126-135)
       d.range = ~d.low & (TOP16 - 1);
       d.low <<= 8;
       d.range <<= 8;
-      if (w.fill < 2) {
-        win_append(w);
-        w.pend = gload16(w.pnx);
-      }
-      d.x = (d.x << 8) | (win_peek(w) >> 24);
-      win_adv(w, 1);
-      d.used += 1;
+      const u32 byte = (d.D0 >> (8 * (d.cpos & 3u))) & 255u;  // D0 holds the byte at cpos
+      d.xhi = __builtin_amdgcn_alignbyte(d.xhi, d.xlo, 3);
+      d.xlo = (d.xlo << 8) | byte;
+      win_step(d, g, 1);
     }
   }
   return wk.s;
@@ -783,65 +821,64 @@ static __device__ __forceinline__ u32 dec_step(ADec& d, Win& w, l_char* tb, u32 
 
 struct DecLane {
   ADec d;
-  Win w;
+  ACode g;
   bool done;
-  u32 hd, nt, tl, col, k;
+  u32 hd, nt, tl, col, k, a;
   u64 clen;
   uint8_t* op;
   uint16_t* tcol;
 };
 
 // lanes with all their tiles decoded: the tail symbols (per lane) and the flag
-static __device__ __forceinline__ void dec_lane_end(DecLane& L, l_char* tb, const AdaptParams& p, u32 t,
-                                    u32* flags) {
+template <int SM>
+static __device__ __forceinline__ void dec_lane_end(DecLane& L, const AdaptParams& p, u32 t,
+                                                    u32* flags) {
   for (u32 j = 0; j < L.tl; ++j) {
     const u32 i = L.hd + 16 * t + j;
-    gstore8(L.op + i, dec_step<false>(L.d, L.w, tb, L.col, L.tcol, p, (i & p.pmask) == p.pmask));
+    gstore8(L.op + i,
+            dec_step<false, SM>(L.d, L.g, L.col, L.tcol, p, (i & p.pmask) == p.pmask));
   }
   // shift_left_buffer panics once more bytes are needed than the stream holds (decoder.rs:33)
-  flags[L.k] = (u64)L.d.used > L.clen ? RC_F_TRUNCATED : 0u;
+  flags[L.k] = (u64)(L.d.cpos - L.a) > L.clen ? RC_F_TRUNCATED : 0u;
   L.done = true;
 }
 
-template <bool UNI>
-static __device__ __forceinline__ void dec_tiles(DecLane& L, l_char* tb, const AdaptParams& p, u32 T, u32 hd_u,
-                                 u32* flags) {
+template <bool UNI, int SM>
+static __device__ __forceinline__ void dec_tiles(DecLane& L, const AdaptParams& p, u32 T,
+                                                 u32 hd_u, u32* flags) {
   for (u32 t = 0; t < T; ++t) {
     if (__any((int)(!L.done && t == L.nt))) {
-      if (!L.done && t == L.nt) dec_lane_end(L, tb, p, t, flags);
+      if (!L.done && t == L.nt) dec_lane_end<SM>(L, p, t, flags);
     }
     const u32 i0 = hd_u + 16 * t;
     const u32 dd = (p.pmask - (L.hd + 16 * t)) & p.pmask;
     u32 o[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      if ((j & 7) == 0) {  // window phase: consume pend (the only wait), load the next block
-        if (L.w.fill <= 4) win_append(L.w);
-        L.w.pend = gload16(L.w.pnx);
-      }
       bool at;
       if (UNI)
         at = ((i0 + j) & p.pmask) == p.pmask;
-      else
-        at = !L.done && ((u32)j & p.pmask) == dd;
-      o[j >> 2] |= dec_step<UNI>(L.d, L.w, tb, L.col, L.tcol, p, at) << (8 * (j & 3));
+      else  // lanes past their chunk's end halve too: it keeps every total below 2^16, which
+            // the magic-table loads rely on
+        at = ((u32)j & p.pmask) == dd;
+      o[j >> 2] |= dec_step<UNI, SM>(L.d, L.g, L.col, L.tcol, p, at) << (8 * (j & 3));
     }
     if (!L.done) gstore128(L.op + L.hd + 16 * t, (u32x4){o[0], o[1], o[2], o[3]});
   }
-  if (!L.done) dec_lane_end(L, tb, p, T, flags);
+  if (!L.done) dec_lane_end<SM>(L, p, T, flags);
 }
 
+template <int SM>
 __global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_decode_adaptive(
     AdaptParams p, const uint8_t* __restrict__ code, const u64* __restrict__ code_off,
     const u64* __restrict__ code_len, uint8_t* __restrict__ syms_out,
     const u64* __restrict__ sym_off, u32 n_chunks, u32* __restrict__ flags) {
   extern __shared__ uint16_t s_tree[];
-  l_char* tb = (l_char*)s_tree;
   const u32 lane = threadIdx.x;
   DecLane L;
   L.k = blockIdx.x * AWG + lane;
   const bool live = L.k < n_chunks;
-  RC_VGPR_FLOOR_144();
+  RC_VGPR_FLOOR_128();
   u64 n = 0;
   L.clen = 0;
   const uint8_t* cp = code;
@@ -868,48 +905,29 @@ __global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   ADec& d = L.d;
   d.total = p.n;
   d.tf = (float)p.n;
-  d.rt = recip(p.n);
+  d.M = gload64(p.magic + p.n);
+  d.Mn = gload64(p.magic + (p.n + p.inc));
   d.low = 0;
   d.range = ~0ull;
-  d.used = 8;
 
-  // code window: the first two 16-B blocks, from the dword holding the first byte
-  Win& w = L.w;
+  // code: origin = the dword holding the first byte; lanes without a stream read g_zero16
   const bool has = !L.done;
-  const u32x4* b0 = has ? (const u32x4*)((uintptr_t)cp & ~(uintptr_t)15) : &g_zero16;
-  w.plast = has ? (const u32x4*)((uintptr_t)(cp + L.clen - 1) & ~(uintptr_t)15) : b0;
+  L.a = has ? (u32)((uintptr_t)cp & 3u) : 0u;
+  L.g.o = has ? cp - L.a : (const uint8_t*)&g_zero16;
+  // n <= 2^25 symbols consume at most 8 + 12 n < 2^29 bytes: code past 2^32 - 256 is never read
+  const u64 cl = min(L.clen, (u64)0xFFFFFF00u);
+  L.g.dwl = has ? (u32)((L.a + cl - 1) & ~3ull) : 12u;
   {
-    const u32x4 B0 = gload16(b0);
-    const u32x4 B1 = gload16(b0 < w.plast ? b0 + 1 : w.plast);
-    const u32 sh = ((u32)(uintptr_t)cp >> 2) & 3u;
-    // r = (B0, B1) shifted down by sh dwords: a barrel shifter (by 1, then by 2)
-    const bool s1 = (sh & 1u) != 0, s2 = (sh & 2u) != 0;
-    const u32 a0 = s1 ? B0.y : B0.x, a1 = s1 ? B0.z : B0.y, a2 = s1 ? B0.w : B0.z;
-    const u32 a3 = s1 ? B1.x : B0.w, a4 = s1 ? B1.y : B1.x, a5 = s1 ? B1.z : B1.y;
-    const u32 a6 = s1 ? B1.w : B1.z, a7 = s1 ? 0u : B1.w;
-    w.r[0] = s2 ? a2 : a0;
-    w.r[1] = s2 ? a3 : a1;
-    w.r[2] = s2 ? a4 : a2;
-    w.r[3] = s2 ? a5 : a3;
-    w.r[4] = s2 ? a6 : a4;
-    w.r[5] = s2 ? a7 : a5;
-    w.r[6] = s2 ? 0u : a6;
-    w.r[7] = s2 ? 0u : a7;
-    w.fill = 8 - sh;
-    w.off = (u32)(uintptr_t)cp & 3u;
-    w.pnx = b0 + 2 <= w.plast ? b0 + 2 : w.plast;
-    w.pend = gload16(w.pnx);
-    // Decoder::new primes 8 bytes (decoder.rs:14-23): two whole dwords from the read position
-    const u32 d0 = win_peek(w);
-#pragma unroll
-    for (int i = 0; i < 7; ++i) w.r[i] = w.r[i + 1];
-    const u32 d1 = win_peek(w);
-#pragma unroll
-    for (int i = 0; i < 7; ++i) w.r[i] = w.r[i + 1];
-    w.fill -= 2;
-    d.x = ((u64)d0 << 32) | d1;  // data - low with low = 0
+    // Decoder::new primes 8 bytes (decoder.rs:14-23), big-endian: dwords 0-2 from the origin
+    const u32 w0 = ldw(L.g, 0), w1 = ldw(L.g, min(4u, L.g.dwl)), w2 = ldw(L.g, min(8u, L.g.dwl));
+    d.xhi = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, L.a));  // data - low, low = 0
+    d.xlo = __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, L.a));
+    d.cpos = L.a + 8;  // (cpos & ~3) = 8
+    d.D0 = w2;
+    d.D1 = ldw(L.g, min(12u, L.g.dwl));
+    d.d2o = min(16u, L.g.dwl);
+    d.D2 = ldw(L.g, d.d2o);
   }
-  dec_preread(d, tb, L.col);
 
   // output: symbols [0, hd) until it is 16-B aligned (per lane, byte stores), nt 16-symbol
   // tiles, then tl symbols
@@ -919,15 +937,16 @@ __global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   L.tl = live ? (u32)((n - L.hd) & 15u) : 0u;
   for (u32 j = 0; __any((int)(j < L.hd && !L.done)); ++j) {
     if (j < L.hd && !L.done) {
-      gstore8(L.op + j, dec_step<false>(d, w, tb, L.col, L.tcol, p, (j & p.pmask) == p.pmask));
+      gstore8(L.op + j,
+              dec_step<false, SM>(d, L.g, L.col, L.tcol, p, (j & p.pmask) == p.pmask));
     }
   }
   const u32 T = wave_max(L.done ? 0u : L.nt);
   const u32 hmin = wave_min(L.done ? 16u : L.hd), hmax = wave_max(L.done ? 0u : L.hd);
   if (hmin >= hmax)
-    dec_tiles<true>(L, tb, p, T, hmax, flags);
+    dec_tiles<true, SM>(L, p, T, hmax, flags);
   else
-    dec_tiles<false>(L, tb, p, T, 0, flags);
+    dec_tiles<false, SM>(L, p, T, 0, flags);
 }
 
 hipError_t rc_adaptive_encode_launch(hipStream_t stream, const AdaptParams& p,
@@ -944,8 +963,14 @@ hipError_t rc_adaptive_decode_launch(hipStream_t stream, const AdaptParams& p,
                                      const uint8_t* code, const u64* code_off,
                                      const u64* code_len, uint8_t* syms_out, const u64* sym_off,
                                      u32 n_chunks, u32* flags) {
-  hipLaunchKernelGGL(k_decode_adaptive, dim3((n_chunks + AWG - 1) / AWG), dim3(AWG),
-                     TREE_BYTES, stream, p, code, code_off, code_len, syms_out, sym_off,
-                     n_chunks, flags);
+  // 256-symbol models keep total >= 256 (every count >= 1), so r < 2^56: 24-bit high products
+  if (p.n == 256)
+    hipLaunchKernelGGL(k_decode_adaptive<1>, dim3((n_chunks + AWG - 1) / AWG), dim3(AWG),
+                       TREE_BYTES, stream, p, code, code_off, code_len, syms_out, sym_off,
+                       n_chunks, flags);
+  else
+    hipLaunchKernelGGL(k_decode_adaptive<0>, dim3((n_chunks + AWG - 1) / AWG), dim3(AWG),
+                       TREE_BYTES, stream, p, code, code_off, code_len, syms_out, sym_off,
+                       n_chunks, flags);
   return hipGetLastError();
 }

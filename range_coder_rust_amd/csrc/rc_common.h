@@ -61,6 +61,7 @@ typedef __attribute__((address_space(1))) u32 g_u32;
 typedef __attribute__((address_space(1))) u64 g_u64;
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 static __device__ __forceinline__ u32 gload(const u32* p) { return *(const g_u32*)p; }
+static __device__ __forceinline__ u64 gload64(const u64* p) { return *(const g_u64*)p; }
 static __device__ __forceinline__ u32x4 gload16(const u32x4* p) { return *(const g_u32x4*)p; }
 static __device__ __forceinline__ void gstore8(uint8_t* p, u32 v) { *(g_u8*)p = (uint8_t)v; }
 static __device__ __forceinline__ void gstore32(uint8_t* p, u32 v) { *(g_u32*)p = v; }
@@ -80,6 +81,7 @@ struct AdaptParams {
   u32 inc;    // count increment per coded symbol
   u32 limit;  // halve the counts when the total exceeds this ...
   u32 pmask;  // ... at every period-th symbol (period = pmask + 1, a power of two)
+  const u64* magic;  // [65536]: floor((2^64 - 1) / t) for range / t (model-owned, device)
 };
 
 // rc_adaptive.hip: launches on `stream`; validate arguments before calling

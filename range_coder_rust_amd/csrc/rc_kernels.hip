@@ -356,11 +356,25 @@ rc_status rc_model_create_adaptive(rc_ctx* ctx, uint32_t n_symbols, uint32_t inc
   if (n_symbols < 1 || n_symbols > 256 || increment < 1 || period < 1 || period > 65536 ||
       (period & (period - 1)) != 0 || grow + n_symbols > limit || limit + grow > 65535)
     return RC_E_BAD_MODEL;
+  // range_par_total (range_coder.rs:38-40) divides by a total that changes every symbol: the
+  // kernels multiply by floor((2^64 - 1) / total) from this table (exact after one correction)
+  std::vector<u64> magic(65536, 0);
+  for (u32 t = 1; t < 65536; ++t) magic[t] = ~0ull / t;
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return RC_E_DEVICE;
+  void* d = nullptr;
+  if (hipMalloc(&d, magic.size() * sizeof(u64)) != hipSuccess) return RC_E_DEVICE;
+  if (hipMemcpy(d, magic.data(), magic.size() * sizeof(u64), hipMemcpyHostToDevice) !=
+      hipSuccess) {
+    (void)hipFree(d);
+    return RC_E_DEVICE;
+  }
   rc_model* mm = new rc_model;
   memset(mm, 0, sizeof *mm);
   mm->kind = 1;
   mm->device = ctx->device;
-  mm->ap = AdaptParams{n_symbols, increment, limit, period - 1};
+  mm->dmem = d;
+  mm->ap = AdaptParams{n_symbols, increment, limit, period - 1, (const u64*)d};
   mm->period = period;
   *out = mm;
   return RC_OK;
