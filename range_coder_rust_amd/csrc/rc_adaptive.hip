@@ -81,23 +81,6 @@ static __device__ __forceinline__ u64 div_magic(u64 v, u32 t, u64 M) {
   return q + (1u + (u32)((int)(rem - t) >> 31));
 }
 
-// (m & a) | (~m & b) for a mask m of 0 / ~0: one v_bfi_b32.  The empty asm hides that m is a
-// mask, or the compiler turns this back into v_cmp + v_cndmask_b32 on VCC.
-static __device__ __forceinline__ u32 msel(u32 m, u32 a, u32 b) {
-  u32 r;  // written out: from the C form the compiler narrows selects of u16 tree values to
-          // 16-bit xor / and / bitop3 sequences and re-extends their results
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-  return r;
-}
-
-// the sign of v as a mask (0 / ~0), opaque to the compiler (which otherwise turns selects on it
-// back into v_cmp + v_cndmask_b32 on VCC)
-static __device__ __forceinline__ u32 smask(u32 v) {
-  u32 r;
-  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(v));
-  return r;
-}
-
 // u32 -> f64 as the single instruction (the compiler widens (double)hi32(x) into a u64
 // conversion: a second convert and an f64 add)
 static __device__ __forceinline__ double cvt_f64(u32 v) {

@@ -53,6 +53,24 @@ static __device__ __forceinline__ u64 sub64(u32 alo, u32 ahi, u64 b) {
   return ((u64)hi << 32) | lo;
 }
 
+// (m & a) | (~m & b) for a mask m of 0 / ~0: one v_bfi_b32, written out.  From the C form the
+// compiler turns selects on masks back into v_cmp + v_cndmask_b32 on VCC (a VALU read of VCC
+// costs ~13 extra SIMD cycles), or narrows selects of u16 values to 16-bit
+// xor / and / bitop3 sequences and re-extends their results.
+static __device__ __forceinline__ u32 msel(u32 m, u32 a, u32 b) {
+  u32 r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+
+// the sign of v as a mask (0 / ~0), opaque to the compiler (which otherwise turns selects on it
+// back into v_cmp + v_cndmask_b32 on VCC)
+static __device__ __forceinline__ u32 smask(u32 v) {
+  u32 r;
+  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
 // Global (not flat) memory access.  A flat access also counts in lgkmcnt, so every LDS wait
 // would wait for it too; pointers that pass through LDS or integer casts lose their address
 // space and compile to flat unless cast back like this.

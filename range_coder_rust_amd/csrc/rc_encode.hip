@@ -160,9 +160,13 @@ static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint
   e.range <<= nb;
   // push: the slot of the dword that was incomplete before this symbol gets the 32 bits above
   // the (new) incomplete ones; if it is still incomplete the slot is rewritten later
-  const u32 slot = __builtin_amdgcn_ubfe(e.B, 5, 5);  // (B >> 5) & (ENC_RING - 1): v_bfe_u32
+  // Slot (B >> 5) & (ENC_RING - 1) sits at byte 256 slot of the column: (B & 0x3E0) << 3, an and
+  // plus one v_lshl_add_u32 (written out: the compiler's form is a shift, an and and an add)
+  u32 soff, saddr;
+  asm("v_and_b32 %0, %1, %2" : "=v"(soff) : "i"((ENC_RING - 1) << 5), "v"(e.B));
+  asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(saddr) : "v"(soff), "v"(e.ring));
   e.B += nb;
-  ring_put(e.ring, slot, (u32)(e.acc >> (e.B & 31u)));
+  *(__attribute__((address_space(3))) u32*)(uintptr_t)saddr = (u32)(e.acc >> (e.B & 31u));
   // SM: range >= 2^32 after narrowing, so the high halves differ (z <= 31) and at most 3 bytes
   // settle; only range_reduction_expansion can be pending
   if (SM) return hi32(e.range) < 0x10000u;

@@ -288,9 +288,11 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
     }
     lut[b] = s | (s1 << 8) | (split << 16);
   }
-  // pad to a power of two (the kernel masks the bucket index) with the last bucket
+  // pad to a power of two (the kernel masks the bucket index) with the last bucket: 2^LUT_BITS
+  // entries whenever total > 2048 (the decoder extracts LUT_BITS bits of the hint)
   while (lut.size() & (lut.size() - 1)) lut.push_back(lut.back());
   a.lut_max = (u32)lut.size() - 1;
+  if (total_freq > 2048 && lut.size() != LUT_MAX_ENTRIES) return RC_E_BAD_MODEL;  // unreachable
 
   if (total_freq <= 2048) {  // direct table: q -> s | cum << 8 | c << 20
     a.direct = 1;
