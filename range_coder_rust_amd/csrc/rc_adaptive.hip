@@ -76,9 +76,9 @@ static __device__ __forceinline__ u64 div_total(u64 v, u32 t, double rt) {
 // table entry M = floor((2^64 - 1) / t): q = mulhi(v, M) is floor(v / t) or one less (v < 2^64,
 // so v / 2^64 < 1 is all M's truncation can lose), and v - q t < 2t tells which, in 32 bits.
 static __device__ __forceinline__ u64 div_magic(u64 v, u32 t, u64 M) {
-  u64 q = __umul64hi(v, M);
-  const u32 rem = (u32)v - (u32)q * t;  // < 2t: its low 32 bits are the remainder
-  return q + (1u + (u32)((int)(rem - t) >> 31));
+  const u64 q = __umul64hi(v, M);
+  const u32 d = (u32)v - (u32)q * t - t;  // remainder - t (the remainder is < 2t: 32 bits do)
+  return q + (1u + smask(d));             // (an opaque sign mask: no v_cmp + v_cndmask on VCC)
 }
 
 // u32 -> f64 as the single instruction (the compiler widens (double)hi32(x) into a u64
@@ -651,10 +651,12 @@ static __device__ __forceinline__ void dec_preread(ADec& d, u32 col) {
 // the crossing lanes makes the compiler copy that register, and wait for the load to do it.
 static __device__ __forceinline__ void win_step(ADec& d, const ACode& g, u32 nb) {
   const u32 c2 = d.cpos + nb;
-  const u32 mc = smask((d.cpos ^ c2) << 29);  // ~0: crossed into the next dword
+  u32 mc, d2n;  // mc = ~0: crossed into the next dword (bit 2 of the position flipped)
+  asm("v_bfe_i32 %0, %1, 2, 1" : "=v"(mc) : "v"(d.cpos ^ c2));
   d.D0 = msel(mc, d.D1, d.D0);
   d.D1 = msel(mc, d.D2, d.D1);
-  d.d2o = min(d.d2o + (mc & 4u), g.dwl);
+  asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(d2n) : "v"(mc), "v"(d.d2o));  // d2o + 4 if crossed
+  d.d2o = min(d2n, g.dwl);
   d.D2 = ldw(g, d.d2o);
   d.cpos = c2;
 }
@@ -727,6 +729,9 @@ static __device__ __forceinline__ u32 dec_step(ADec& d, const ACode& g, u32 col,
   // range / total.  (Read at the end of the previous symbol and carried instead, they are
   // re-zero-extended by the compiler at the loop latch, which also waits for them there.)
   dec_preread(d, col);
+  // (kept here by a scheduling barrier: left to itself the scheduler issues these reads just
+  // before the walk needs them, after the hint and the division, and waits for them there)
+  __builtin_amdgcn_sched_barrier(0);
   // hint q ~ x * total / range from the high halves (range >= 2^48: relative error <= 2^-15),
   // clamped to total - 1: the walk's upper-end tracking relies on q < total
   const float X = cvt_f32(d.xhi), R = cvt_f32(hi32(d.range));
