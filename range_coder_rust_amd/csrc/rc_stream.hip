@@ -3,11 +3,28 @@
 //
 // rc_encode_host / rc_decode_host replace n_chunks x {Encoder::new; encode...; finish}
 // (src/encoder.rs:14-46) / {Decoder::new; decode...} (src/decoder.rs:14-54) for data that lives
-// in host memory.  The chunks are cut into batches of ~RC_STREAM_BATCH_BYTES; batch b runs on
-// stream b % RC_STREAM_SLOTS with that slot's device buffers, so the copy engines move batch
-// b+1 in and batch b-1 out while batch b is coded.  The caller's big buffers are page-locked in
-// place for the call (hipHostRegister; already pinned memory is used as it is), so every copy
-// is a direct DMA.  PCIe, not HBM, bounds this path: ~50 GB/s each way on Gen5 x16.
+// in host memory.  The chunks are cut into batches of ~RC_STREAM_BATCH_BYTES; batch b uses slot
+// b % RC_STREAM_SLOTS's device buffers.  Two streams:
+//  * the in stream moves batch inputs host -> HBM with the DMA engines (hipMemcpyAsync), running
+//    up to RC_STREAM_SLOTS batches ahead;
+//  * the coder stream codes batch b, then moves its output HBM -> host with a copy kernel
+//    (k_pcie_copy) that writes the mapped host buffer.
+// The caller's big buffers are page-locked in place for the call (hipHostRegister; already
+// pinned memory is used as it is) and mapped into the device's address space.  PCIe, not HBM,
+// bounds this path.
+//
+// Why this split (tools/pcie_duplex.py, tools/pcie_kernel_probe.hip on the MI355X boxes):
+//  * the DMA engines move 57 GB/s one way, but only 28.7 GB/s each way when H2D and D2H run at
+//    once, which is a pipeline's steady state;
+//  * copy kernels keep 45-47 GB/s each way at once, but while they touch host memory every other
+//    kernel's HBM loads stall (a latency-bound probe kernel: 2.4 ms alone, 30-47 ms beside copy
+//    kernels of 16-256 workgroups, on disjoint CUs too; a decode batch: 9.7 -> 36 ms);
+//  * DMA H2D (31.6 GB/s) beside a D2H copy kernel (50.6 GB/s) is 82 GB/s together, and DMA
+//    traffic leaves the coder alone (probe kernel 2.85 ms).
+// So the coder never runs beside a copy kernel, and the DMA engines refill the input slots the
+// whole time.  Each batch is staged in HBM at its host ranges' addresses mod 64, so the copy
+// kernel moves 16-B vectors on both sides whatever the caller's alignment.  RC_STREAM_DMA=1 (or
+// memory that cannot be mapped) moves outputs with hipMemcpyAsync too.
 #include "rc_common.h"
 
 #include <stdlib.h>
@@ -20,10 +37,16 @@
 #include <unordered_map>
 #include <vector>
 
-#define RC_STREAM_SLOTS 4
-// A chunk is one lane's serial stream: a batch kernel takes ~10-20 ms whatever its size, so a
-// batch must carry ~1 GiB for the coder to outrun PCIe (~50 GB/s x 20 ms).
-#define RC_STREAM_BATCH_BYTES (1ull << 30)
+#define RC_STREAM_SLOTS 3
+// A chunk is one lane's serial stream: a batch kernel takes ~7-15 ms whatever its size (up to
+// ~20 GiB of 64 KiB chunks, when every SIMD holds its 5 waves), and the coder stream pays it
+// once per batch beside ~20 ms of output copy per GiB, so batches are large: 2 GiB, with the
+// first two at 1/4 and 1/2 of that so the first input copy is short.
+#define RC_STREAM_BATCH_BYTES (2ull << 30)
+#define RC_STEP_COPIES 4  // copies per launch of k_pcie_copy (a batch's output: data, lengths,
+                          // flags)
+#define RC_COPY_WGS 256   // workgroups per bulk copy (tools/pcie_kernel_probe.hip: 256 keeps
+                          // 46.7 GB/s each way with both directions at once; 2048 drops to 33)
 
 struct rc_ctx;
 struct rc_model;
@@ -53,7 +76,7 @@ thread_local bool t_pinned_by_caller = false;
 struct Pin {
   void* p = nullptr;
   bool mine = false;
-  Pin(const void* ptr, size_t n, unsigned flags = hipHostRegisterDefault) {
+  Pin(const void* ptr, size_t n, unsigned flags = hipHostRegisterMapped) {
     if (!ptr || !n || t_pinned_by_caller) return;
     p = const_cast<void*>(ptr);
     mine = hipHostRegister(p, n, flags) == hipSuccess;
@@ -64,16 +87,118 @@ struct Pin {
   }
 };
 
+// device address of a pinned host byte (nullptr: not mapped, use the DMA engines)
+const uint8_t* mapped(const void* host) {
+  void* d = nullptr;
+  if (!host || hipHostGetDevicePointer(&d, const_cast<void*>(host), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return (const uint8_t*)d;
+}
+
+bool use_dma() {
+  const char* e = getenv("RC_STREAM_DMA");
+  return e && *e && *e != '0';
+}
+
+struct CopyArgs {
+  const uint8_t* src[RC_STEP_COPIES];
+  uint8_t* dst[RC_STEP_COPIES];
+  u64 n[RC_STEP_COPIES];
+};
+
+// copy blockIdx.y of a step: n bytes, one side mapped host memory.  When (src & 15) == (dst & 15)
+// (bulk data: staging follows the host address) the body moves 16-B vectors, 4 per lane in
+// flight, and the first wave copies the unaligned head and tail; otherwise (offset and result
+// arrays, a few KiB) it copies bytes.
+__global__ __launch_bounds__(256) void k_pcie_copy(CopyArgs a) {
+  const uint8_t* __restrict__ src = a.src[blockIdx.y];
+  uint8_t* __restrict__ dst = a.dst[blockIdx.y];
+  const u64 n = a.n[blockIdx.y];
+  if (((uintptr_t)src ^ (uintptr_t)dst) & 15) {
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256)
+      dst[i] = src[i];
+    return;
+  }
+  const u64 head = min(n, (u64)((16u - ((u32)(uintptr_t)dst & 15u)) & 15u));
+  const u64 n16 = (n - head) >> 4, tail = (n - head) & 15;
+  const uint4* s4 = (const uint4*)(src + head);
+  uint4* d4 = (uint4*)(dst + head);
+  const u64 stride = (u64)gridDim.x * 1024;
+  for (u64 i = (u64)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + 256 * u < n16) v[u] = s4[i + 256 * u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + 256 * u < n16) d4[i + 256 * u] = v[u];
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 32) {
+    const u32 t = threadIdx.x;
+    if (t < head) dst[t] = src[t];
+    if (t >= 16 && t - 16 < tail) {
+      const u64 o = head + 16 * n16 + (t - 16);
+      dst[o] = src[o];
+    }
+  }
+}
+
+// one copy of a step; the host side's device address hdev is nullptr when it is not mapped
+struct Copy {
+  uint8_t* dst;
+  const uint8_t* src;
+  u64 n;
+  bool h2d;
+  const uint8_t* hdev;
+};
+
+// issue a step's copies on s: one k_pcie_copy launch for all mapped ones, hipMemcpyAsync for
+// the rest
+bool copy_step(const std::vector<Copy>& cs, hipStream_t s) {
+  CopyArgs a{};
+  u32 k = 0;
+  u64 nmax = 0;
+  for (const Copy& c : cs) {
+    if (c.n == 0) continue;
+    if (!c.hdev) {
+      if (hipMemcpyAsync(c.dst, c.src, c.n,
+                         c.h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, s) != hipSuccess)
+        return false;
+      continue;
+    }
+    a.src[k] = c.h2d ? c.hdev : c.src;
+    a.dst[k] = c.h2d ? c.dst : const_cast<uint8_t*>(c.hdev);
+    a.n[k] = c.n;
+    nmax = std::max(nmax, c.n);
+    ++k;
+  }
+  if (k == 0) return true;
+  static const u64 wgs = [] {
+    const char* e = getenv("RC_STREAM_COPY_WGS");
+    return e && atoi(e) > 0 ? (u64)atoi(e) : (u64)RC_COPY_WGS;
+  }();
+  const unsigned gx = (unsigned)std::min<u64>(wgs, (nmax + 16383) / 16384);
+  hipLaunchKernelGGL(k_pcie_copy, dim3(gx, k), dim3(256), 0, s, a);
+  return hipGetLastError() == hipSuccess;
+}
+
 struct Batch {
   u32 k0, k1;       // chunks [k0, k1)
   u64 in0, in1;     // input byte range (host)
   u64 out0, out1;   // output byte range (host)
+  u64 mi, mo;       // staging displacement: the host ranges' addresses mod 64
+  u64* ho;          // its offsets in the pinned offset array
 };
 
-// Resources of the pipeline: RC_STREAM_SLOTS streams, each with its own device buffers, and
-// one pinned array for every batch's relative offsets and per-chunk results.
+// Resources of the pipeline: RC_STREAM_SLOTS sets of device buffers, the copy and coder
+// streams, per-slot events, and one pinned array for every batch's relative offsets and
+// per-chunk results.
 struct Pipe {
-  hipStream_t st[RC_STREAM_SLOTS] = {};
+  hipStream_t copy = nullptr, code = nullptr;  // in stream (DMA), coder + out stream
+  hipEvent_t copied[RC_STREAM_SLOTS] = {};  // batch t's input is in HBM (slot t % SLOTS)
+  hipEvent_t coded[RC_STREAM_SLOTS] = {};   // batch t is coded and out (slot t % SLOTS)
   uint8_t* din[RC_STREAM_SLOTS] = {};
   uint8_t* dout[RC_STREAM_SLOTS] = {};
   u64* doff[RC_STREAM_SLOTS] = {};  // [2 * (kmax + 1)] offsets + [kmax] lengths
@@ -93,8 +218,10 @@ struct Pipe {
   bool init(size_t in_max, size_t out_max, u32 kmax, u32 n_chunks, size_t n_off) {
     (void)hipGetDevice(&device);
     c_in = in_max, c_out = out_max, c_k = kmax, c_n = n_chunks, c_off = n_off;
+    ok = ok && make_streams();
     for (int i = 0; i < RC_STREAM_SLOTS; ++i) {
-      ok = ok && hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(&copied[i], hipEventDisableTiming) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(&coded[i], hipEventDisableTiming) == hipSuccess;
       ok = ok && hipMalloc((void**)&din[i], in_max + 64) == hipSuccess;
       ok = ok && hipMalloc((void**)&dout[i], out_max + 64) == hipSuccess;
       ok = ok && hipMalloc((void**)&doff[i], 8ull * (3ull * kmax + 2)) == hipSuccess;
@@ -105,10 +232,14 @@ struct Pipe {
     ok = ok && hipHostMalloc((void**)&hfl, 4ull * n_chunks + 4, hipHostMallocDefault) == hipSuccess;
     return ok;
   }
+  bool make_streams() {
+    return hipStreamCreateWithFlags(&copy, hipStreamNonBlocking) == hipSuccess &&
+           hipStreamCreateWithFlags(&code, hipStreamNonBlocking) == hipSuccess;
+  }
   bool drain() {
     bool r = true;
-    for (int i = 0; i < RC_STREAM_SLOTS; ++i)
-      if (st[i]) r = hipStreamSynchronize(st[i]) == hipSuccess && r;
+    if (copy) r = hipStreamSynchronize(copy) == hipSuccess && r;
+    if (code) r = hipStreamSynchronize(code) == hipSuccess && r;
     return r;
   }
   ~Pipe() {
@@ -118,8 +249,11 @@ struct Pipe {
       if (dout[i]) (void)hipFree(dout[i]);
       if (doff[i]) (void)hipFree(doff[i]);
       if (dfl[i]) (void)hipFree(dfl[i]);
-      if (st[i]) (void)hipStreamDestroy(st[i]);
+      if (copied[i]) (void)hipEventDestroy(copied[i]);
+      if (coded[i]) (void)hipEventDestroy(coded[i]);
     }
+    if (copy) (void)hipStreamDestroy(copy);
+    if (code) (void)hipStreamDestroy(code);
     if (hoff) (void)hipHostFree(hoff);
     if (hlen) (void)hipHostFree(hlen);
     if (hfl) (void)hipHostFree(hfl);
@@ -195,14 +329,15 @@ u64 batch_bytes() {
   return v ? v : RC_STREAM_BATCH_BYTES;
 }
 
-// cut [0, n) into batches of about batch_bytes() of input (>= 1 chunk each)
+// cut [0, n) into batches of about batch_bytes() of input (>= 1 chunk each; the first two
+// of 1/4 and 1/2 of that)
 template <class InRange, class OutRange>
 std::vector<Batch> plan(u32 n, InRange in_range, OutRange out_range) {
-  const u64 cap = batch_bytes();
   std::vector<Batch> b;
   u32 k = 0;
   while (k < n) {
-    Batch x;
+    const u64 cap = batch_bytes() >> (b.size() < 2 ? 2 - b.size() : 0);
+    Batch x{};
     x.k0 = k;
     u64 lo, hi, olo, ohi;
     in_range(k, lo, hi);
@@ -231,6 +366,30 @@ rc_status any_flag(const uint32_t* flags, uint32_t n) {
   return RC_OK;
 }
 
+// Run the pipeline over B batches: batch t's input moves in on p.copy once batch t - SLOTS is
+// out (its slot free), then p.code codes it and moves its output out.
+template <class In, class Code, class Out>
+rc_status run_pipeline(Pipe& p, size_t B, In in, Code code, Out out) {
+  std::vector<Copy> cs;
+  for (size_t t = 0; t < B; ++t) {
+    const int i = (int)(t % RC_STREAM_SLOTS);
+    cs.clear();
+    if (t >= RC_STREAM_SLOTS && hipStreamWaitEvent(p.copy, p.coded[i], 0) != hipSuccess)
+      return RC_E_DEVICE;
+    in(t, i, cs);
+    if (!copy_step(cs, p.copy) || hipEventRecord(p.copied[i], p.copy) != hipSuccess ||
+        hipStreamWaitEvent(p.code, p.copied[i], 0) != hipSuccess)
+      return RC_E_DEVICE;
+    const rc_status st = code(t, i);
+    if (st != RC_OK) return st;
+    cs.clear();
+    out(t, i, cs);
+    if (!copy_step(cs, p.code) || hipEventRecord(p.coded[i], p.code) != hipSuccess)
+      return RC_E_DEVICE;
+  }
+  return p.drain() ? RC_OK : RC_E_DEVICE;
+}
+
 }  // namespace
 
 extern "C" {
@@ -248,7 +407,7 @@ rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   DevSet g(dev);
   // a chunk the kernel flags RC_F_TOO_LONG (never read nor written) is staged as empty
   auto too_long = [&](u32 k) { return sym_off[k + 1] - sym_off[k] > RC_MAX_CHUNK_SYMBOLS; };
-  const std::vector<Batch> bs = plan(
+  std::vector<Batch> bs = plan(
       n_chunks,
       [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = too_long(k) ? a : sym_off[k + 1]; },
       [&](u32 k, u64& a, u64& b) { a = out_off[k], b = too_long(k) ? a : out_off[k + 1]; });
@@ -263,42 +422,50 @@ rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   // (the pins outlive the lease, whose destructor drains the streams on every return path)
   Pin pin_in(syms + sym_off[0], sym_off[n_chunks] - sym_off[0]);
   Pin pin_out(out + out_off[0], out_off[n_chunks] - out_off[0]);
+  const bool dma = use_dma();
+  const uint8_t* const m_out = dma ? nullptr : mapped(out + out_off[0]);
   PipeLease lease{ctx, pipe_acquire(ctx, dev, in_max, out_max, kmax, n_chunks, n_off)};
   if (!lease.p) return RC_E_DEVICE;
   Pipe& p = *lease.p;
+  const uint8_t* const m_len = m_out ? mapped(p.hlen) : nullptr;
+  const uint8_t* const m_fl = m_out ? mapped(p.hfl) : nullptr;
   // the caller's stream must not run ahead into our buffers, nor we into its pending work
   (void)hipStreamSynchronize(s0);
   size_t o = 0;
-  for (size_t bi = 0; bi < bs.size(); ++bi) {
-    const Batch& b = bs[bi];
-    const int i = (int)(bi % RC_STREAM_SLOTS);
-    hipStream_t s = p.st[i];
+  auto in = [&](size_t t, int i, std::vector<Copy>& cs) {
+    Batch& b = bs[t];
     const u32 nk = b.k1 - b.k0;
-    u64* ho = p.hoff + o;  // [sym_off rel (nk+1)] [out_off rel (nk+1)]
+    b.mi = (uintptr_t)(syms + b.in0) & 63, b.mo = (uintptr_t)(out + b.out0) & 63;
+    u64* ho = b.ho = p.hoff + o;  // [sym_off rel (nk+1)] [out_off rel (nk+1)]
     for (u32 j = 0; j <= nk; ++j) {
-      ho[j] = sym_off[b.k0 + j] - b.in0;
-      ho[nk + 1 + j] = out_off[b.k0 + j] - b.out0;
+      ho[j] = sym_off[b.k0 + j] - b.in0 + b.mi;
+      ho[nk + 1 + j] = out_off[b.k0 + j] - b.out0 + b.mo;
     }
     o += 2ull * (nk + 1);
-    bool ok = hipMemcpyAsync(p.din[i], syms + b.in0, b.in1 - b.in0, hipMemcpyHostToDevice, s) ==
-                  hipSuccess &&
-              hipMemcpyAsync(p.doff[i], ho, 16ull * (nk + 1), hipMemcpyHostToDevice, s) == hipSuccess;
-    if (!ok) return RC_E_DEVICE;
-    u64* d_soff = p.doff[i];
-    u64* d_ooff = p.doff[i] + (nk + 1);
-    u64* d_len = p.doff[i] + 2 * (nk + 1);
-    if (rc_ctx_set_stream(ctx, s) != RC_OK) return RC_E_DEVICE;
-    const rc_status st = rc_encode_batch(ctx, m, p.din[i], d_soff, nk, p.dout[i], d_ooff, d_len,
-                                         p.dfl[i]);
+    cs.push_back({p.din[i] + b.mi, syms + b.in0, b.in1 - b.in0, true, nullptr});
+    cs.push_back({(uint8_t*)p.doff[i], (const uint8_t*)ho, 16ull * (nk + 1), true, nullptr});
+  };
+  auto code = [&](size_t t, int i) {
+    const Batch& b = bs[t];
+    const u32 nk = b.k1 - b.k0;
+    if (rc_ctx_set_stream(ctx, p.code) != RC_OK) return RC_E_DEVICE;
+    const rc_status st = rc_encode_batch(ctx, m, p.din[i], p.doff[i], nk, p.dout[i],
+                                         p.doff[i] + (nk + 1), p.doff[i] + 2 * (nk + 1), p.dfl[i]);
     (void)rc_ctx_set_stream(ctx, s0);
-    if (st != RC_OK) return st;
-    ok = hipMemcpyAsync(out + b.out0, p.dout[i], b.out1 - b.out0, hipMemcpyDeviceToHost, s) ==
-             hipSuccess &&
-         hipMemcpyAsync(p.hlen + b.k0, d_len, 8ull * nk, hipMemcpyDeviceToHost, s) == hipSuccess &&
-         hipMemcpyAsync(p.hfl + b.k0, p.dfl[i], 4ull * nk, hipMemcpyDeviceToHost, s) == hipSuccess;
-    if (!ok) return RC_E_DEVICE;
-  }
-  if (!p.drain()) return RC_E_DEVICE;
+    return st;
+  };
+  auto outc = [&](size_t t, int i, std::vector<Copy>& cs) {
+    const Batch& b = bs[t];
+    const u32 nk = b.k1 - b.k0;
+    cs.push_back({out + b.out0, p.dout[i] + b.mo, b.out1 - b.out0, false,
+                  m_out ? m_out + (b.out0 - out_off[0]) : nullptr});
+    cs.push_back({(uint8_t*)(p.hlen + b.k0), (const uint8_t*)(p.doff[i] + 2 * (nk + 1)), 8ull * nk,
+                  false, m_len ? m_len + 8ull * b.k0 : nullptr});
+    cs.push_back({(uint8_t*)(p.hfl + b.k0), (const uint8_t*)p.dfl[i], 4ull * nk, false,
+                  m_fl ? m_fl + 4ull * b.k0 : nullptr});
+  };
+  const rc_status st = run_pipeline(p, bs.size(), in, code, outc);
+  if (st != RC_OK) return st;
   memcpy(out_len, p.hlen, 8ull * n_chunks);
   memcpy(flags, p.hfl, 4ull * n_chunks);
   return any_flag(flags, n_chunks);
@@ -316,7 +483,7 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
     if (sym_off[k + 1] < sym_off[k]) return RC_E_ARG;
   DevSet g(dev);
   auto too_long = [&](u32 k) { return sym_off[k + 1] - sym_off[k] > RC_MAX_CHUNK_SYMBOLS; };
-  const std::vector<Batch> bs = plan(
+  std::vector<Batch> bs = plan(
       n_chunks,
       [&](u32 k, u64& a, u64& b) { a = code_off[k], b = too_long(k) ? a : a + code_len[k]; },
       [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = too_long(k) ? a : sym_off[k + 1]; });
@@ -333,39 +500,47 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   }
   Pin pin_in(code + cmin, cmax - cmin);
   Pin pin_out(syms_out + sym_off[0], sym_off[n_chunks] - sym_off[0]);
+  const bool dma = use_dma();
+  const uint8_t* const m_out = dma ? nullptr : mapped(syms_out + sym_off[0]);
   PipeLease lease{ctx, pipe_acquire(ctx, dev, in_max, out_max, kmax, n_chunks, n_off)};
   if (!lease.p) return RC_E_DEVICE;
   Pipe& p = *lease.p;
+  const uint8_t* const m_fl = m_out ? mapped(p.hfl) : nullptr;
   (void)hipStreamSynchronize(s0);
   size_t o = 0;
-  for (size_t bi = 0; bi < bs.size(); ++bi) {
-    const Batch& b = bs[bi];
-    const int i = (int)(bi % RC_STREAM_SLOTS);
-    hipStream_t s = p.st[i];
+  auto in = [&](size_t t, int i, std::vector<Copy>& cs) {
+    Batch& b = bs[t];
     const u32 nk = b.k1 - b.k0;
-    u64* ho = p.hoff + o;  // [code_off rel (nk) | code_len (nk)] [sym_off rel (nk+1)]
+    b.mi = (uintptr_t)(code + b.in0) & 63, b.mo = (uintptr_t)(syms_out + b.out0) & 63;
+    u64* ho = b.ho = p.hoff + o;  // [code_off rel (nk) | code_len (nk)] [sym_off rel (nk+1)]
     for (u32 j = 0; j < nk; ++j) {
-      ho[j] = code_off[b.k0 + j] - b.in0;
+      ho[j] = code_off[b.k0 + j] - b.in0 + b.mi;
       ho[nk + j] = code_len[b.k0 + j];
     }
-    for (u32 j = 0; j <= nk; ++j) ho[2 * nk + j] = sym_off[b.k0 + j] - b.out0;
+    for (u32 j = 0; j <= nk; ++j) ho[2 * nk + j] = sym_off[b.k0 + j] - b.out0 + b.mo;
     o += 3ull * nk + 1;
-    bool ok = hipMemcpyAsync(p.din[i], code + b.in0, b.in1 - b.in0, hipMemcpyHostToDevice, s) ==
-                  hipSuccess &&
-              hipMemcpyAsync(p.doff[i], ho, 8ull * (3ull * nk + 1), hipMemcpyHostToDevice, s) ==
-                  hipSuccess;
-    if (!ok) return RC_E_DEVICE;
-    if (rc_ctx_set_stream(ctx, s) != RC_OK) return RC_E_DEVICE;
+    cs.push_back({p.din[i] + b.mi, code + b.in0, b.in1 - b.in0, true, nullptr});
+    cs.push_back({(uint8_t*)p.doff[i], (const uint8_t*)ho, 8ull * (3ull * nk + 1), true, nullptr});
+  };
+  auto coder = [&](size_t t, int i) {
+    const Batch& b = bs[t];
+    const u32 nk = b.k1 - b.k0;
+    if (rc_ctx_set_stream(ctx, p.code) != RC_OK) return RC_E_DEVICE;
     const rc_status st = rc_decode_batch(ctx, m, p.din[i], p.doff[i], p.doff[i] + nk, p.dout[i],
                                          p.doff[i] + 2 * nk, nk, p.dfl[i]);
     (void)rc_ctx_set_stream(ctx, s0);
-    if (st != RC_OK) return st;
-    ok = hipMemcpyAsync(syms_out + b.out0, p.dout[i], b.out1 - b.out0, hipMemcpyDeviceToHost,
-                        s) == hipSuccess &&
-         hipMemcpyAsync(p.hfl + b.k0, p.dfl[i], 4ull * nk, hipMemcpyDeviceToHost, s) == hipSuccess;
-    if (!ok) return RC_E_DEVICE;
-  }
-  if (!p.drain()) return RC_E_DEVICE;
+    return st;
+  };
+  auto outc = [&](size_t t, int i, std::vector<Copy>& cs) {
+    const Batch& b = bs[t];
+    const u32 nk = b.k1 - b.k0;
+    cs.push_back({syms_out + b.out0, p.dout[i] + b.mo, b.out1 - b.out0, false,
+                  m_out ? m_out + (b.out0 - sym_off[0]) : nullptr});
+    cs.push_back({(uint8_t*)(p.hfl + b.k0), (const uint8_t*)p.dfl[i], 4ull * nk, false,
+                  m_fl ? m_fl + 4ull * b.k0 : nullptr});
+  };
+  const rc_status st = run_pipeline(p, bs.size(), in, coder, outc);
+  if (st != RC_OK) return st;
   memcpy(flags, p.hfl, 4ull * n_chunks);
   return any_flag(flags, n_chunks);
 }
@@ -422,8 +597,9 @@ rc_status rc_encode_host_multi(rc_ctx* const* ctxs, const rc_model* const* model
   for (u32 k = 0; k < n_chunks; ++k)
     if (sym_off[k + 1] < sym_off[k] || out_off[k + 1] < out_off[k]) return RC_E_ARG;
   // pinned once for every device (each device's call then finds its range already pinned)
-  Pin pin_in(syms + sym_off[0], sym_off[n_chunks] - sym_off[0], hipHostRegisterPortable);
-  Pin pin_out(out + out_off[0], out_off[n_chunks] - out_off[0], hipHostRegisterPortable);
+  const unsigned pf = hipHostRegisterPortable | hipHostRegisterMapped;
+  Pin pin_in(syms + sym_off[0], sym_off[n_chunks] - sym_off[0], pf);
+  Pin pin_out(out + out_off[0], out_off[n_chunks] - out_off[0], pf);
   const std::vector<u32> cut =
       split_by_bytes(n_chunks, n_ctx, [&](u32 k) { return sym_off[k + 1] - sym_off[k]; });
   return run_parts(n_ctx, cut, [&](u32 i, u32 k0, u32 nk) {
@@ -448,8 +624,9 @@ rc_status rc_decode_host_multi(rc_ctx* const* ctxs, const rc_model* const* model
     cmin = std::min(cmin, code_off[k]);
     cmax = std::max(cmax, code_off[k] + code_len[k]);
   }
-  Pin pin_in(code + cmin, cmax - cmin, hipHostRegisterPortable);
-  Pin pin_out(syms_out + sym_off[0], sym_off[n_chunks] - sym_off[0], hipHostRegisterPortable);
+  const unsigned pf = hipHostRegisterPortable | hipHostRegisterMapped;
+  Pin pin_in(code + cmin, cmax - cmin, pf);
+  Pin pin_out(syms_out + sym_off[0], sym_off[n_chunks] - sym_off[0], pf);
   const std::vector<u32> cut = split_by_bytes(n_chunks, n_ctx, [&](u32 k) { return code_len[k]; });
   return run_parts(n_ctx, cut, [&](u32 i, u32 k0, u32 nk) {
     return rc_decode_host(ctxs[i], models[i], code, code_off + k0, code_len + k0, syms_out,

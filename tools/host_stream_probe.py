@@ -42,6 +42,8 @@ def main():
         print(f"rep {rep}: encode {t1 - t0:.3f} s ({n * L / (t1 - t0) / 1e9:.1f} GB/s), "
               f"decode {t2 - t1:.3f} s ({n * L / (t2 - t1) / 1e9:.1f} GB/s), "
               f"ok={bool((fl == 0).all() and (fd == 0).all())}", flush=True)
+        if rep == 0:
+            print("round trip exact:", bool(np.array_equal(dec, syms)), flush=True)
 
 
 if __name__ == "__main__":
