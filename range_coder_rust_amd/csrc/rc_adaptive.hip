@@ -283,18 +283,44 @@ typedef __attribute__((address_space(3))) char l_char;
 #define LRD(tb, a) ((u32) * (const __attribute__((address_space(3))) uint16_t*)(uintptr_t)(a))
 #define LWR(tb, a, v) (*(__attribute__((address_space(3))) uint16_t*)(uintptr_t)(a) = (uint16_t)(v))
 
-static __device__ __forceinline__ void esym_prep(ESym& q, u32 s, u32 col) {
+// The turn-bit words of every symbol value (bs, bs1, nbm of ESym; 48 B per symbol, 12 KiB):
+// three 16-B loads from this L1-resident table replace ~20 shifts and masks per symbol in the
+// model wave, whose instruction count bounds the encoder.  They are loaded two symbols ahead
+// (ETurn), so their latency stays off the symbol chain.
+struct ETurnTable {
+  u32 w[256][12];
+};
+static constexpr ETurnTable make_turn_table() {
+  ETurnTable t{};
+  for (u32 s = 0; s < 256; ++s) {
+    const u32 u = s | (s << 15), s1 = s + 1, u1 = s1 | (s1 << 15);
+    for (int k = 0; k < 4; ++k) {
+      t.w[s][k] = (u >> (6 - 2 * k)) & 0x10001u;
+      t.w[s][4 + k] = (u1 >> (6 - 2 * k)) & 0x10001u;
+      t.w[s][8 + k] = t.w[s][k] ^ 0x10001u;
+    }
+  }
+  return t;
+}
+__device__ const ETurnTable g_turn_table = make_turn_table();
+
+struct ETurn {
+  u32x4 b0, b1, b2;
+};
+static __device__ __forceinline__ ETurn eturn_load(u32 s) {
+  const u32x4* t = (const u32x4*)g_turn_table.w[s];
+  return ETurn{gload16(t), gload16(t + 1), gload16(t + 2)};
+}
+
+// symbol s, whose turn bits tb were loaded earlier
+static __device__ __forceinline__ void esym_prep(ESym& q, u32 s, u32 col, const ETurn& t) {
   const u32 X = (s << 7) | col;
 #pragma unroll
   for (int l = 0; l < 8; ++l) q.a[l] = X & LMASK(l);
-  const u32 u = s | (s << 15), s1 = s + 1, u1 = s1 | (s1 << 15);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    q.bs[k] = (u >> (6 - 2 * k)) & 0x10001u;
-    q.bs1[k] = (u1 >> (6 - 2 * k)) & 0x10001u;
-    q.nbm[k] = q.bs[k] ^ 0x10001u;
-  }
-  q.s1hi = s1 >> 8;
+  q.bs[0] = t.b0.x, q.bs[1] = t.b0.y, q.bs[2] = t.b0.z, q.bs[3] = t.b0.w;
+  q.bs1[0] = t.b1.x, q.bs1[1] = t.b1.y, q.bs1[2] = t.b1.z, q.bs1[3] = t.b1.w;
+  q.nbm[0] = t.b2.x, q.nbm[1] = t.b2.y, q.nbm[2] = t.b2.z, q.nbm[3] = t.b2.w;
+  q.s1hi = (s + 1) >> 8;
   q.s = s;
 }
 
@@ -312,8 +338,8 @@ static __device__ __forceinline__ void esym_code(const ESym& q, l_char* tb, u32 
   for (int k = 0; k < 4; ++k)
     vp[k] = (us2){(unsigned short)q.v[2 * k + 1], (unsigned short)q.v[2 * k]};
   u32 a0 = __builtin_amdgcn_udot2(vp[0], __builtin_bit_cast(us2, q.bs[0]), 0u, false);
-  u32 a1 = __builtin_amdgcn_udot2(vp[0], __builtin_bit_cast(us2, q.bs1[0]), q.s1hi * total,
-                                  false);
+  u32 a1 = __builtin_amdgcn_udot2(vp[0], __builtin_bit_cast(us2, q.bs1[0]),
+                                  __umul24(q.s1hi, total), false);
 #pragma unroll
   for (int k = 1; k < 4; ++k) {
     a0 = __builtin_amdgcn_udot2(vp[k], __builtin_bit_cast(us2, q.bs[k]), a0, false);
@@ -385,10 +411,10 @@ static __device__ __forceinline__ void funnel4(u32 (&w)[4], const u32x4& b0, con
 // the same symbol index, so the period's halving check is a scalar test.  The next symbol's
 // tree reads are issued while the current one finishes, after the halving check.
 template <int H>
-static __device__ __forceinline__ void model_step(ESym& q, u32& total, const u32 (&w)[2],
-                                                  u32 wn, u32 t, uint16_t* tcol, l_char* tb,
-                                                  u32 col, u32 lane, us2 incp,
-                                                  const AdaptParams& p) {
+static __device__ __forceinline__ void model_step(ESym& q, ETurn& tn, u32& total,
+                                                  const u32 (&w)[2], u32 wn, u32 t,
+                                                  uint16_t* tcol, l_char* tb, u32 col, u32 lane,
+                                                  us2 incp, const AdaptParams& p) {
 #pragma unroll
   for (int j = 0; j < FIFO_SYMS; ++j) {
     u32 cum, c;
@@ -403,8 +429,11 @@ static __device__ __forceinline__ void model_step(ESym& q, u32& total, const u32
       }
     }
     const u32 sn = j < 7 ? (w[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 255u : wn & 255u;
+    const u32 s2 = j + 2 < 8 ? (w[(j + 2) >> 2] >> (8 * ((j + 2) & 3))) & 255u
+                             : (wn >> (8 * (j - 6))) & 255u;
     ESym qn;
-    esym_prep(qn, sn, col);
+    esym_prep(qn, sn, col, tn);  // tn: symbol sn's turn bits, loaded a symbol ago
+    tn = eturn_load(s2);
     esym_load(qn, tb);
     // bit 31: a symbol outside the alphabet (the reference panics, sample_impl.rs:19), where
     // the coder stops; c >= 1 keeps entries codable for lanes past their chunk's end
@@ -429,33 +458,42 @@ static __device__ __forceinline__ void model_wave(const AdaptParams& p, const ui
   const u32 blast = has ? (u32)((mis + n - 1) >> 4) : 0u;  // last block holding a symbol
   auto blk = [&](u32 u) -> u32x4 { return gload16(has ? bp + min(u, blast) : &g_zero16); };
   const u32 m0 = 0u - ((mis >> 2) & 1u), m1 = 0u - ((mis >> 3) & 1u);
-  u32x4 B1 = blk(1), B2 = blk(2);
+  // blocks g + 1 and g + 2 are in registers (or in flight) while group g is modelled; the block
+  // loaded during group g is first needed a group later
+  u32x4 Ba = blk(1), Bb = blk(2);
   u32 nw[4];
-  funnel4(nw, blk(0), B1, m0, m1, mis);  // group 0
+  funnel4(nw, blk(0), Ba, m0, m1, mis);  // group 0
   ESym q;
-  esym_prep(q, nw[0] & 255u, col);
+  esym_prep(q, nw[0] & 255u, col, eturn_load(nw[0] & 255u));
   esym_load(q, tb);
-  // one 16-symbol group (two steps) per iteration, a barrier after each step: T + 1 barriers
-  // in all, as in the coder wave
-  for (u32 t = 0; t <= T; t += 2) {
+  ETurn tn = eturn_load((nw[0] >> 8) & 255u);
+  // group t / 2 (two steps), a barrier after each step: T + 1 barriers in all, as in the coder
+  // wave.  Bx = block t/2 + 1, By = block t/2 + 2; Bx is then reloaded with block t/2 + 3.
+  auto group = [&](u32 t, u32x4& Bx, const u32x4& By) {
     u32 cw[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) cw[k] = nw[k];
     if (t < T) {
-      funnel4(nw, B1, B2, m0, m1, mis);  // the next group (its first symbol is looked ahead)
-      B1 = B2;
-      B2 = blk((t >> 1) + 3);
+      funnel4(nw, Bx, By, m0, m1, mis);  // the next group (its first symbol is looked ahead)
+      Bx = blk((t >> 1) + 3);
       const u32 wa[2] = {cw[0], cw[1]};
-      model_step<0>(q, total, wa, cw[2], t, tcol, tb, col, lane, incp, p);
+      model_step<0>(q, tn, total, wa, cw[2], t, tcol, tb, col, lane, incp, p);
     }
     __syncthreads();
     if (t + 1 <= T) {
       if (t + 1 < T) {
         const u32 wb[2] = {cw[2], cw[3]};
-        model_step<1>(q, total, wb, nw[0], t + 1, tcol, tb, col, lane, incp, p);
+        model_step<1>(q, tn, total, wb, nw[0], t + 1, tcol, tb, col, lane, incp, p);
       }
       __syncthreads();
     }
+  };
+  // two groups per iteration, the two block registers swapping roles: a loop-carried rotation
+  // (B1 = B2; B2 = load) made the compiler copy the new load at the loop latch and wait there
+  // for it, a whole HBM latency per 16 symbols
+  for (u32 t = 0; t <= T; t += 4) {
+    group(t, Ba, Bb);
+    if (t + 2 <= T) group(t + 2, Bb, Ba);
   }
 }
 
