@@ -113,6 +113,7 @@ struct CopyArgs {
 // flight, and the first wave copies the unaligned head and tail; otherwise (offset and result
 // arrays, a few KiB) it copies bytes.
 __global__ __launch_bounds__(256) void k_pcie_copy(CopyArgs a) {
+  RC_VGPR_FLOOR_32();  // (build() requires allocations in 16-register steps)
   const uint8_t* __restrict__ src = a.src[blockIdx.y];
   uint8_t* __restrict__ dst = a.dst[blockIdx.y];
   const u64 n = a.n[blockIdx.y];
