@@ -159,3 +159,35 @@ def test_host_multi_device_list_equals_single(ctx):
     for k in (0, n // 2, n - 1):
         f, b, lb = cpu.encode(c, cum, total, syms[soff[k]: soff[k + 1]])
         assert f == 0 and out3[ooff[k]: ooff[k] + lb].tobytes() == b
+
+
+@pytest.mark.parametrize("dma", ["0", "1"])
+def test_output_copy_paths_on_offset_pinned_buffers(ctx, monkeypatch, dma):
+    """Outputs leave by the copy kernel (mapped host memory) or, with RC_STREAM_DMA=1, by DMA;
+    both byte-exact, on pinned buffers used at odd offsets (interior mapped pointers, staging
+    displaced to the host address mod 64) across several batches."""
+    monkeypatch.setenv("RC_STREAM_DMA", dma)
+    monkeypatch.setenv("RC_STREAM_BATCH_BYTES", "300000")
+    rng = np.random.default_rng(29)
+    c, cum, total = synth.zipf_table()
+    m = rc.StaticModel(c, cum, total)
+    n = 96
+    lens, soff = layout(rng, n, 0, 20000, gap=True)
+    nsym = int(soff[-1])
+    pin_in = torch.empty(nsym + 64, dtype=torch.uint8, pin_memory=True).numpy()
+    syms = pin_in[5:5 + nsym]
+    syms[:] = rng.choice(256, nsym, p=np.asarray(c, float) / np.sum(c)).astype(np.uint8)
+    caps = np.array([rc.slot_capacity(int(L), m.max_bits_per_symbol()) for L in lens])
+    ooff = np.concatenate([[0], caps]).cumsum()
+    pin_out = torch.empty(int(ooff[-1]) + 64, dtype=torch.uint8, pin_memory=True).numpy()
+    out = pin_out[3:3 + int(ooff[-1])]
+    out, ol, fl = rc.encode_host(m, syms, soff, ooff, out=out)
+    assert (fl == 0).all()
+    for k in range(n):
+        f, b, L = cpu.encode(c, cum, total, syms[soff[k]: soff[k + 1]])
+        assert f == 0 and ol[k] == L and bytes(out[ooff[k]: ooff[k] + L]) == b, k
+    pin_dec = torch.empty(nsym - int(soff[0]) + 64, dtype=torch.uint8, pin_memory=True).numpy()
+    dsoff = soff - soff[0]
+    dec = pin_dec[7:7 + int(dsoff[-1])]
+    dec, fd = rc.decode_host(m, out, ooff[:-1], ol, dsoff, out=dec)
+    assert (fd == 0).all() and (dec == syms[soff[0]: soff[-1]]).all()
