@@ -161,12 +161,14 @@ def test_host_multi_device_list_equals_single(ctx):
         assert f == 0 and out3[ooff[k]: ooff[k] + lb].tobytes() == b
 
 
-@pytest.mark.parametrize("dma", ["0", "1"])
-def test_output_copy_paths_on_offset_pinned_buffers(ctx, monkeypatch, dma):
-    """Outputs leave by the copy kernel (mapped host memory) or, with RC_STREAM_DMA=1, by DMA;
-    both byte-exact, on pinned buffers used at odd offsets (interior mapped pointers, staging
-    displaced to the host address mod 64) across several batches."""
+@pytest.mark.parametrize("dma,direct", [("0", "1"), ("0", "0"), ("1", "1")])
+def test_output_copy_paths_on_offset_pinned_buffers(ctx, monkeypatch, dma, direct):
+    """Outputs written by the coder straight into mapped host memory (default), staged and moved
+    by the copy kernel (RC_STREAM_DIRECT=0), or moved by DMA (RC_STREAM_DMA=1): all byte-exact,
+    on pinned buffers used at odd offsets (interior mapped pointers, staging displaced to the
+    host address mod 64) across several batches."""
     monkeypatch.setenv("RC_STREAM_DMA", dma)
+    monkeypatch.setenv("RC_STREAM_DIRECT", direct)
     monkeypatch.setenv("RC_STREAM_BATCH_BYTES", "300000")
     rng = np.random.default_rng(29)
     c, cum, total = synth.zipf_table()
