@@ -193,3 +193,24 @@ def test_output_copy_paths_on_offset_pinned_buffers(ctx, monkeypatch, dma, direc
     dec = pin_dec[7:7 + int(dsoff[-1])]
     dec, fd = rc.decode_host(m, out, ooff[:-1], ol, dsoff, out=dec)
     assert (fd == 0).all() and (dec == syms[soff[0]: soff[-1]]).all()
+
+
+def test_adaptive_model_through_host_path(ctx, monkeypatch):
+    """The host pipeline with the adaptive (C4) model: ragged chunks across several batches,
+    every stream byte-exact vs the adaptive oracle and the round trip exact."""
+    monkeypatch.setenv("RC_STREAM_BATCH_BYTES", "40000")
+    rng = np.random.default_rng(41)
+    m = rc.AdaptiveModel(256, 32, 57343, 256)
+    n = 40
+    lens, soff = layout(rng, n, 0, 6000)
+    w = 1.0 / np.arange(1, 257) ** 1.2
+    syms = rng.choice(256, int(soff[-1]), p=w / w.sum()).astype(np.uint8)
+    caps = np.array([rc.slot_capacity(int(L), 16) for L in lens])
+    ooff = np.concatenate([[0], caps]).cumsum()
+    out, ol, fl = rc.encode_host(m, syms, soff, ooff)
+    assert (fl == 0).all()
+    for k in range(n):
+        f, b, L = cpu.encode_adaptive(256, 32, 57343, 256, syms[soff[k]: soff[k + 1]])
+        assert f == 0 and ol[k] == L and bytes(out[ooff[k]: ooff[k] + L]) == b, k
+    dec, fd = rc.decode_host(m, out, ooff[:-1], ol, soff)
+    assert (fd == 0).all() and (dec == syms).all()
