@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 
@@ -245,22 +246,28 @@ struct Dev {
 // demand and kept until rc_ctx_destroy.  Every transfer is one DMA between the two (pageable
 // caller memory is only touched by host memcpy), so copies and the kernel are plainly ordered
 // on the context's stream.  (Small async copies to and from pageable memory returned wrong
-// bytes intermittently on this stack; pinned staging is also the faster path.)  A context is
-// used by one host thread at a time (include/range_coder.h), so its block needs no lock.
+// bytes intermittently on this stack; pinned staging is also the faster path.)  The block is
+// held under its own mutex for the whole call: the Python mirrors share one default context
+// between threads, and ctypes releases the GIL inside the call.
 struct Stage {
+  std::mutex mu;
   char* host = nullptr;
   char* dev = nullptr;
   size_t cap = 0;
 };
 std::mutex g_stage_mu;
-std::unordered_map<const rc_ctx*, Stage> g_stages;
+std::unordered_map<const rc_ctx*, std::unique_ptr<Stage>> g_stages;
 
-char* stage_acquire(const rc_ctx* ctx, size_t bytes, char** dev) {
+// Locks the context's block (released when `lk` goes out of scope) and grows it to `bytes`.
+char* stage_acquire(const rc_ctx* ctx, size_t bytes, char** dev, std::unique_lock<std::mutex>* lk) {
   Stage* st;
   {
-    std::lock_guard<std::mutex> lk(g_stage_mu);
-    st = &g_stages[ctx];
+    std::lock_guard<std::mutex> g(g_stage_mu);
+    auto& slot = g_stages[ctx];
+    if (!slot) slot.reset(new Stage);
+    st = slot.get();
   }
+  *lk = std::unique_lock<std::mutex>(st->mu);
   if (st->cap < bytes) {
     if (st->host) (void)hipHostFree(st->host);
     if (st->dev) (void)hipFree(st->dev);
@@ -278,6 +285,10 @@ char* stage_acquire(const rc_ctx* ctx, size_t bytes, char** dev) {
   *dev = st->dev;
   return st->host;
 }
+
+// Above this many worst-case output bytes, rc_stream_encode_host reads back the state first and
+// then only the bytes written (two waits); below it one copy of the whole region is cheaper.
+constexpr u64 kTwoPhaseBytes = 256u << 10;
 
 }  // namespace
 
@@ -338,7 +349,8 @@ rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint3
   const size_t o_off = 64, o_len = o_off + 32, o_fl = o_len + 16, o_tr = o_fl + 16;
   const size_t o_nb = o_tr + ((12 * n + 15) & ~15ull), o_out = o_nb + ((n + 15) & ~15ull);
   char* d = nullptr;
-  char* h = stage_acquire(ctx, o_out + need, &d);
+  std::unique_lock<std::mutex> lk;
+  char* h = stage_acquire(ctx, o_out + need, &d, &lk);
   if (!h) return RC_E_DEVICE;
   memcpy(h, state, sizeof *state);
   const u64 offs[4] = {0, n, 0, need};  // sym_off[0..1], out_off[0..1]
@@ -351,19 +363,33 @@ rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint3
                      nbytes ? (uint8_t*)(d + o_nb) : (uint8_t*)nullptr, finish,
                      (u32*)(d + o_fl));
   if (hipGetLastError() != hipSuccess) return RC_E_DEVICE;
-  // state, out_len and flags, then the new bytes and counts
-  if (hipMemcpyAsync(h, d, o_tr, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(h + o_nb, d + o_nb, o_out + need - o_nb, hipMemcpyDeviceToHost, s) !=
-          hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return RC_E_DEVICE;
+  // state, out_len and flags, then the new bytes (and the counts, when asked for).  A large
+  // call reads the state first and then only the w bytes written, not the 12n + 8 worst case.
+  const bool two_phase = need > kTwoPhaseBytes;
+  if (hipMemcpyAsync(h, d, o_tr, hipMemcpyDeviceToHost, s) != hipSuccess) return RC_E_DEVICE;
+  if (!two_phase) {
+    if ((nbytes && n &&
+         hipMemcpyAsync(h + o_nb, d + o_nb, n, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (need && hipMemcpyAsync(h + o_out, d + o_out, need, hipMemcpyDeviceToHost, s) !=
+                     hipSuccess))
+      return RC_E_DEVICE;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return RC_E_DEVICE;
   rc_stream_state nst;
   memcpy(&nst, h, sizeof nst);
   u64 w;
   u32 fl;
   memcpy(&w, h + o_len, 8);
   memcpy(&fl, h + o_fl, 4);
-  if (w > need) return RC_E_DEVICE;
+  if (w > need || nst.n - state->n > n) return RC_E_DEVICE;
+  if (two_phase) {
+    const u64 got = nst.n - state->n;
+    if ((nbytes && got &&
+         hipMemcpyAsync(h + o_nb, d + o_nb, got, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (w && hipMemcpyAsync(h + o_out, d + o_out, w, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return RC_E_DEVICE;
+  }
   if (w) memcpy(out, h + o_out, w);
   if (nbytes && n) memcpy(nbytes, h + o_nb, nst.n - state->n);
   *state = nst;
@@ -391,7 +417,8 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
   const size_t o_off = 64, o_fl = o_off + 32, o_c = o_fl + 16, o_cum = o_c + 1024;
   const size_t o_win = o_cum + 1024, o_sym = o_win + ((wlen + 15) & ~15ull);
   char* d = nullptr;
-  char* h = stage_acquire(ctx, o_sym + n, &d);
+  std::unique_lock<std::mutex> lk;
+  char* h = stage_acquire(ctx, o_sym + n, &d, &lk);
   if (!h) return RC_E_DEVICE;
   rc_stream_state rel = *state;
   rel.pos -= p0;  // the window starts at p0 (stage 0: at the stream start)
@@ -428,16 +455,17 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
 
 // internal: free the context's staging block (called by rc_ctx_destroy)
 void rc_resume_release_(const rc_ctx* ctx) {
-  Stage st;
+  std::unique_ptr<Stage> st;
   {
     std::lock_guard<std::mutex> lk(g_stage_mu);
     auto it = g_stages.find(ctx);
     if (it == g_stages.end()) return;
-    st = it->second;
+    st = std::move(it->second);
     g_stages.erase(it);
   }
-  if (st.host) (void)hipHostFree(st.host);
-  if (st.dev) (void)hipFree(st.dev);
+  std::lock_guard<std::mutex> lk(st->mu);  // a call still inside the block finishes first
+  if (st->host) (void)hipHostFree(st->host);
+  if (st->dev) (void)hipFree(st->dev);
 }
 
 }  // extern "C"

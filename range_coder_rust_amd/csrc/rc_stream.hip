@@ -340,9 +340,11 @@ u64 batch_bytes() {
 }
 
 // cut [0, n) into batches of about batch_bytes() of input (>= 1 chunk each; the first two
-// of 1/4 and 1/2 of that)
-template <class InRange, class OutRange>
-std::vector<Batch> plan(u32 n, InRange in_range, OutRange out_range) {
+// of 1/4 and 1/2 of that).  A chunk for which alone(k) holds (one the kernel flags
+// RC_F_TOO_LONG without reading or writing it) is a batch of its own, so no batch's input or
+// output range spans its bytes.
+template <class InRange, class OutRange, class Alone>
+std::vector<Batch> plan(u32 n, InRange in_range, OutRange out_range, Alone alone) {
   std::vector<Batch> b;
   u32 k = 0;
   while (k < n) {
@@ -354,7 +356,7 @@ std::vector<Batch> plan(u32 n, InRange in_range, OutRange out_range) {
     out_range(k, olo, ohi);
     x.in0 = lo, x.in1 = hi, x.out0 = olo, x.out1 = ohi;
     ++k;
-    while (k < n) {
+    while (k < n && !alone(k - 1) && !alone(k)) {
       u64 a, c, oa, oc;
       in_range(k, a, c);
       out_range(k, oa, oc);
@@ -420,7 +422,8 @@ rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   std::vector<Batch> bs = plan(
       n_chunks,
       [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = too_long(k) ? a : sym_off[k + 1]; },
-      [&](u32 k, u64& a, u64& b) { a = out_off[k], b = too_long(k) ? a : out_off[k + 1]; });
+      [&](u32 k, u64& a, u64& b) { a = out_off[k], b = too_long(k) ? a : out_off[k + 1]; },
+      too_long);
   size_t in_max = 0, out_max = 0, n_off = 0;
   u32 kmax = 0;
   for (const Batch& b : bs) {
@@ -500,7 +503,8 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   std::vector<Batch> bs = plan(
       n_chunks,
       [&](u32 k, u64& a, u64& b) { a = code_off[k], b = too_long(k) ? a : a + code_len[k]; },
-      [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = too_long(k) ? a : sym_off[k + 1]; });
+      [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = too_long(k) ? a : sym_off[k + 1]; },
+      too_long);
   size_t in_max = 0, out_max = 0, n_off = 0;
   u32 kmax = 0;
   u64 cmin = ~0ull, cmax = 0;

@@ -106,3 +106,33 @@ def test_host_stream_too_long_chunk(ctx):
     assert fl.tolist() == [0, 0, N.F_TOO_LONG] and int(ol[2]) == 0
     dec, fd = rc.decode_host(m, out, ooff[:3], np.array([ol[0], ol[1], 64], np.uint64), soff)
     assert fd.tolist() == [0, 0, N.F_TOO_LONG] and np.array_equal(dec[:200], syms[:200])
+
+
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_host_stream_too_long_chunk_mid_batch(ctx, monkeypatch, direct):
+    """A too-long chunk between in-limit chunks of one batch: its input is not staged and its
+    output slot is not overwritten, on the direct (mapped) and staged output paths."""
+    monkeypatch.setenv("RC_STREAM_DIRECT", direct)
+    m = _models(ctx)["zipf"]
+    rng = np.random.default_rng(4)
+    n_big = MAX + 1
+    syms = np.zeros(200 + n_big + 300, np.uint8)
+    syms[:200] = rng.integers(0, 256, 200).astype(np.uint8)
+    syms[200 + n_big:] = rng.integers(0, 256, 300).astype(np.uint8)
+    e = 200 + n_big
+    soff = np.array([0, 100, 200, e, e + 150, e + 300], np.uint64)
+    ooff = np.arange(6, dtype=np.uint64) * 4096
+    out = np.full(5 * 4096, 0xEE, np.uint8)
+    out, ol, fl = rc.encode_host(m, syms, soff, ooff, out=out)
+    assert fl.tolist() == [0, 0, N.F_TOO_LONG, 0, 0] and int(ol[2]) == 0
+    assert (out[2 * 4096:3 * 4096] == 0xEE).all()  # the flagged slot untouched
+    for k in (0, 1, 3, 4):
+        f, b, lb = cpu.encode(m.c, m.cum, m.total, syms[int(soff[k]):int(soff[k + 1])])
+        assert f == 0 and lb == int(ol[k]) and bytes(out[int(ooff[k]):int(ooff[k]) + lb]) == b
+    code_len = ol.astype(np.uint64).copy()
+    code_len[2] = 64
+    dec = np.full(len(syms), 0xEE, np.uint8)
+    dec, fd = rc.decode_host(m, out, ooff[:5], code_len, soff, out=dec)
+    assert fd.tolist() == [0, 0, N.F_TOO_LONG, 0, 0]
+    assert np.array_equal(dec[:200], syms[:200]) and np.array_equal(dec[e:], syms[e:])
+    assert (dec[200:e] == 0xEE).all()  # the flagged chunk's symbols untouched

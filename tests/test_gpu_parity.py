@@ -344,6 +344,47 @@ def test_coresident_workgroups(ctx, cfg):
         assert f == 0 and lb == ol[k] and bytes(h[k * cap:k * cap + lb]) == b, k
 
 
+@pytest.mark.parametrize("rank", [3])
+def test_n8_rank_shard(ctx, rank):
+    """configs[4] at N = 8: one rank's shard of the 2^20 x 64 KiB Zipf(1.2) stream, i.e. 2^17
+    chunks of 65536 symbols generated as global chunks [rank * 2^17, (rank + 1) * 2^17) of the
+    bench's seed (shard.synth_seed).  512 workgroups: two per CU, the co-residency shape of the
+    8-GPU line.  Every chunk round-trips; 16 chunks, one from each 1/16 of the
+    grid (both workgroups of a CU included), are bit-checked against the oracle."""
+    from range_coder_rust_amd import shard
+    c, cum, total = synth.zipf_table()
+    m = rc.StaticModel(c, cum, total)
+    inv = synth.inverse_cdf(c)
+    n, L = 1 << 17, 1 << 16
+    lo, hi = shard.shard_range(1 << 20, 8, rank)
+    assert hi - lo == n
+    seed = shard.synth_seed(0x5EED0001, lo)
+    syms = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    synth.fill(ctx, seed, inv, syms, L, n)
+    sym_off = torch.arange(n + 1, dtype=torch.int64, device="cuda") * L
+    cap = rc.slot_capacity(L, 6.0, slack=1.02)  # Zipf(1.2) codes at ~5.3 bits/symbol
+    out_off = torch.arange(n + 1, dtype=torch.int64, device="cuda") * cap
+    out = torch.empty(n * cap, dtype=torch.uint8, device="cuda")
+    out_len, flags = rc.encode_batch(m, syms, sym_off, out, out_off)
+    dec = torch.empty_like(syms)
+    fd = rc.decode_batch(m, out, out_off[:-1].contiguous(), out_len, dec, sym_off)
+    torch.cuda.synchronize()
+    assert int(flags.abs().sum()) == 0 and int(fd.abs().sum()) == 0
+    step = 1 << 30
+    for i in range(0, n * L, step):
+        assert torch.equal(dec[i:i + step], syms[i:i + step]), i
+    ol = out_len.cpu().numpy()
+    for j in range(16):
+        k = j * (n // 16) + (j * 4099) % (n // 16)
+        ch = synth.host_chunk(seed, inv, k, L)
+        assert np.array_equal(ch, syms[k * L:(k + 1) * L].cpu().numpy()), k
+        f, b, lb = cpu.encode(c, cum, total, ch)
+        got = bytes(out[k * cap:k * cap + lb].cpu().numpy())
+        assert f == 0 and lb == ol[k] and got == b, k
+    del syms, out, dec
+    torch.cuda.empty_cache()
+
+
 def test_cpp_sample_impl(ctx):
     """The reference example (examples/sample_impl.rs) via the C++ host API (include/*.hpp)."""
     import subprocess

@@ -1,0 +1,138 @@
+"""Build-time check for the gfx950 top-register hazard.
+
+Measured on MI355X (tools/vgpr88, profiles/r03/vgpr88.txt): a 64-bit shift (v_lshlrev_b64,
+v_lshrrev_b64, v_ashrrev_i64) whose 32-bit shift amount is read from the LAST VGPR of the
+wave's allocation returns wrong results on waves whose VGPR block does not start at the bottom
+of the register file, i.e. whenever another wave is resident below it on the same SIMD.  The
+same instructions one register lower, and 32-bit shifts reading that register, are exact.
+
+This module disassembles every gfx950 code object inside a shared library and reports, per
+kernel, its VGPR allocation (from the kernel descriptor), the highest VGPR its code names and
+each 64-bit shift whose amount operand is the allocation's last register.  build() refuses a
+library with any such instruction.
+"""
+import re
+import struct
+import subprocess
+import sys
+import tempfile
+import os
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+SHIFT64 = ("v_lshlrev_b64", "v_lshrrev_b64", "v_ashrrev_i64")
+
+
+def code_objects(lib):
+    """The gfx950 code objects of every offload bundle in lib's .hip_fatbin section."""
+    with tempfile.TemporaryDirectory() as td:
+        fat = os.path.join(td, "fatbin")
+        subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", lib,
+                        os.path.join(td, "copy")], check=True, capture_output=True)
+        data = open(fat, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+        out = []
+        for i, s in enumerate(starts):
+            e = starts[i + 1] if i + 1 < len(starts) else len(data)
+            b = os.path.join(td, f"b{i}")
+            o = os.path.join(td, f"co{i}")
+            open(b, "wb").write(data[s:e])
+            r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o", "--unbundle",
+                                f"--input={b}", f"--targets={TARGET}", f"--output={o}"],
+                               capture_output=True)
+            if r.returncode == 0 and os.path.getsize(o):
+                out.append(open(o, "rb").read())
+        return out
+
+
+def _descriptors(co_path):
+    out = subprocess.run([f"{LLVM}/llvm-readelf", "-S", "-s", "-W", co_path], capture_output=True,
+                         text=True, check=True).stdout
+    data = open(co_path, "rb").read()
+    secs = {}
+    for line in out.splitlines():
+        t = line.strip()
+        if t.startswith("[") and "]" in t:
+            try:
+                idx = int(t[1:t.index("]")])
+            except ValueError:
+                continue
+            parts = t[t.index("]") + 1:].split()
+            if len(parts) >= 4:
+                secs[idx] = (int(parts[2], 16), int(parts[3], 16))
+    alloc = {}
+    for line in out.splitlines():
+        p = line.split()
+        if len(p) >= 8 and p[7].endswith(".kd") and p[6].isdigit():
+            addr = int(p[1], 16)
+            sa, so = secs[int(p[6])]
+            rsrc1 = struct.unpack_from("<I", data, so + addr - sa + 48)[0]
+            alloc[p[7][:-3]] = ((rsrc1 & 63) + 1) * 8
+    return alloc
+
+
+def _vregs(operand):
+    m = re.fullmatch(r"v\[(\d+):(\d+)\]", operand)
+    if m:
+        return list(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.fullmatch(r"v(\d+)", operand)
+    return [int(m.group(1))] if m else []
+
+
+def check_code_object(blob):
+    """{kernel: (alloc, highest named VGPR, [offending instructions])}"""
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "co")
+        open(path, "wb").write(blob)
+        alloc = _descriptors(path)
+        dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", path],
+                             capture_output=True, text=True, check=True).stdout
+    res, cur = {}, None
+    for line in dis.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            cur = m.group(1) if m.group(1) in alloc else None
+            if cur:
+                res[cur] = [alloc[cur], -1, []]
+            continue
+        if not cur:
+            continue
+        text = line.split("//")[0].strip()
+        if not text:
+            continue
+        parts = text.split(None, 1)
+        op = parts[0]
+        args = [a.strip() for a in parts[1].split(",")] if len(parts) > 1 else []
+        for a in args:
+            for r in _vregs(a):
+                res[cur][1] = max(res[cur][1], r)
+        if op.startswith(SHIFT64) and len(args) >= 2:
+            top = res[cur][0] - 1
+            if _vregs(args[1]) == [top]:
+                res[cur][2].append(text)
+    return {k: tuple(v) for k, v in res.items()}
+
+
+def check_library(lib):
+    out = {}
+    for blob in code_objects(lib):
+        out.update(check_code_object(blob))
+    return out
+
+
+def main(lib):
+    res = check_library(lib)
+    bad = 0
+    for k, (alloc, hi, offenders) in sorted(res.items()):
+        flag = "  TOP-REGISTER SHIFT AMOUNT" if offenders else ""
+        print(f"{alloc:4d} {hi + 1:4d}  {k}{flag}")
+        for t in offenders[:4]:
+            print("        ", t)
+        bad += bool(offenders)
+    print(f"{len(res)} kernels, {bad} with a 64-bit shift reading its allocation's last VGPR")
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1]))

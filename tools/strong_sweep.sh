@@ -2,11 +2,13 @@
 # Per-GPU rate of the configs[4] shard sizes on one GPU: the chunk count one rank codes at
 # N = 8, 4, 2, 1 (2^17 .. 2^20 chunks of 64 KiB, Zipf(1.2)).  value x N over value(2^20)
 # predicts the strong-scaling efficiency the 8-GPU run can reach (the ranks share nothing).
-#   gpurun -- 'bash tools/strong_sweep.sh'   -> gpurun_out/strong_<chunks>.json
+#   gpurun -- 'bash tools/strong_sweep.sh [outdir]'   -> <outdir>/strong_<chunks>.json
+# RC_LIB_PATH selects a scratch library build (e.g. variants/librc_amd_dec80.so).
 set -e
-mkdir -p gpurun_out
+out=${1:-gpurun_out}
+mkdir -p "$out"
 for n in 131072 262144 524288 1048576; do
   timeout -k 10 300 python bench.py --config zipf --global-chunks $n --steps 5 --warmup 2 \
-    --no-cpu-baseline > gpurun_out/strong_$n.json 2> gpurun_out/strong_$n.err
+    --no-cpu-baseline > "$out/strong_$n.json" 2> "$out/strong_$n.err"
   echo "$n done"
 done

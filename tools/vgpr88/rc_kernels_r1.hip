@@ -51,6 +51,60 @@ struct ModelArgs {
   float ftotal;      // (float)total
 };
 
+
+#ifdef RC_PROBE
+// Diagnostic side buffers: per wave {HW_ID, GPR_ALLOC, LDS_ALLOC, XCC_ID,
+// t_start lo/hi, t_end lo/hi}; per chunk {changed-canary mask, first changed value}.
+__device__ u32 g_probe[(1u << 17) / 64 * 8 * 4];
+__device__ u32 g_canary[(1u << 17) * 2 * 4];
+#define PROBE_BEGIN()                                                              \
+  if ((tid & 63) == 0) {                                                           \
+    const u64 pr_t0 = wall_clock64();                                              \
+    u32* pp = g_probe + ((blockIdx.x * WG + tid) >> 6) * 8;                        \
+    pp[0] = __builtin_amdgcn_s_getreg(0xF804);                                     \
+    pp[1] = __builtin_amdgcn_s_getreg(0xF805);                                     \
+    pp[2] = __builtin_amdgcn_s_getreg(0xF806);                                     \
+    pp[3] = __builtin_amdgcn_s_getreg(0xF814);                                     \
+    pp[4] = (u32)pr_t0; pp[5] = (u32)(pr_t0 >> 32);                                \
+  }
+#define PROBE_END(k)                                                               \
+  if (((k) & 63) == 0) {                                                           \
+    const u64 pr_t1 = wall_clock64();                                              \
+    u32* pp = g_probe + ((k) >> 6) * 8;                                            \
+    pp[6] = (u32)pr_t1; pp[7] = (u32)(pr_t1 >> 32);                                \
+  }
+#else
+#define PROBE_BEGIN()
+#define PROBE_END(k)
+#endif
+#ifdef RC_CANARY
+// Fill v88..v95 (inside a 96-VGPR allocation, above every register the code names) and read
+// them back at the end: any change means the wave wrote past the registers it names.
+#define CANARY_SET()                                                               \
+  asm volatile("v_mov_b32 v88, 0xca000058\n\tv_mov_b32 v89, 0xca000059\n\t"        \
+               "v_mov_b32 v90, 0xca00005a\n\tv_mov_b32 v91, 0xca00005b\n\t"        \
+               "v_mov_b32 v92, 0xca00005c\n\tv_mov_b32 v93, 0xca00005d\n\t"        \
+               "v_mov_b32 v94, 0xca00005e\n\tv_mov_b32 v95, 0xca00005f" ::          \
+                   : "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95")
+#define CANARY_CHECK(k)                                                            \
+  {                                                                                \
+    u32 cv[8];                                                                     \
+    asm volatile("v_mov_b32 %0, v88\n\tv_mov_b32 %1, v89\n\tv_mov_b32 %2, v90\n\t"  \
+                 "v_mov_b32 %3, v91\n\tv_mov_b32 %4, v92\n\tv_mov_b32 %5, v93\n\t"   \
+                 "v_mov_b32 %6, v94\n\tv_mov_b32 %7, v95"                             \
+                 : "=v"(cv[0]), "=v"(cv[1]), "=v"(cv[2]), "=v"(cv[3]), "=v"(cv[4]),      \
+                   "=v"(cv[5]), "=v"(cv[6]), "=v"(cv[7])::"v88", "v89", "v90", "v91",  \
+                   "v92", "v93", "v94", "v95");                                       \
+    u32 mask = 0, first = 0;                                                       \
+    for (int j = 7; j >= 0; --j)                                                   \
+      if (cv[j] != 0xca000058u + j) mask |= 1u << j, first = cv[j];                \
+    if ((k) < (1u << 17) * 4) g_canary[2 * (k)] = mask, g_canary[2 * (k) + 1] = first; \
+  }
+#else
+#define CANARY_SET()
+#define CANARY_CHECK(k)
+#endif
+
 static __device__ __forceinline__ u32 hi32(u64 v) { return (u32)(v >> 32); }
 
 // RangeCoder::range_par_total (range_coder.rs:38-40): range / total, exact.
@@ -186,6 +240,8 @@ __global__ __launch_bounds__(WG) void k_encode_static(ModelArgs m, const uint8_t
 #ifdef RC_R1_FLOOR96
   asm volatile("; vgpr floor 96" ::: "v95");
 #endif
+  CANARY_SET();
+  PROBE_BEGIN();
   if (k >= n_chunks) return;
 
   const u32 lane = tid & 63, wave = tid >> 6;
@@ -255,6 +311,8 @@ __global__ __launch_bounds__(WG) void k_encode_static(ModelArgs m, const uint8_t
   if (!st.flag && (u64)len > cap) st.flag = RC_F_CAPACITY;
   out_len[k] = len;
   flags[k] = st.flag;
+  CANARY_CHECK(k);
+  PROBE_END(k);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -845,4 +903,11 @@ rc_status rc_synth_fill(rc_ctx* ctx, uint64_t seed, const uint8_t* inv_cdf_host,
   return st;
 }
 
+#ifdef RC_PROBE
+int rc_probe_read(void* probe, size_t probe_bytes, void* canary, size_t canary_bytes) {
+  if (hipMemcpyFromSymbol(probe, HIP_SYMBOL(g_probe), probe_bytes) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(canary, HIP_SYMBOL(g_canary), canary_bytes) != hipSuccess) return -1;
+  return 0;
+}
+#endif
 }  // extern "C"
