@@ -31,10 +31,15 @@ namespace rc {
 
 class RangeCoderError : public std::runtime_error {
  public:
+  // error.rs:3-13: which reference error a BAD_MODEL flag stands for, with its payload
+  enum Kind { OTHER = 0, LOWER_BOUND_OVERFLOW, UPPER_BOUND_OVERFLOW, DIVIDE_BY_ZERO };
   RangeCoderError(const std::string& what, int status = 0, uint32_t flags = 0)
       : std::runtime_error(what), status(status), flags(flags) {}
   int status;      // rc_status of the failing call
   uint32_t flags;  // RC_F_* of the failing chunk (0 if not chunk-specific)
+  Kind kind = OTHER;
+  // LowerBoundOverflow {lower_bound, add_val, range} / UpperBoundOverflow {lower_bound, range}
+  uint64_t lower_bound = 0, add_val = 0, range = 0;
 };
 
 inline void check(rc_status s, const char* what) {
@@ -64,15 +69,19 @@ class Decoder;
 // trait PModel (src/pmodel.rs:4-41)
 class PModel {
  public:
+  static constexpr size_t kCanonical = ~(size_t)0;
   virtual ~PModel() = default;
   virtual uint32_t c_freq(size_t index) const = 0;    // pmodel.rs:6
   virtual uint32_t cum_freq(size_t index) const = 0;  // pmodel.rs:8
   virtual uint32_t total_freq() const = 0;            // pmodel.rs:10
-  // pmodel.rs:12.  The GPU decoder evaluates the canonical inverse cum[s] <= rfreq < cum[s+1]
-  // itself (FreqTable::find_index, sample_impl.rs:27-45); this hook is not called.
-  virtual size_t find_index(const Decoder&) const {
-    throw RangeCoderError("find_index runs inside the GPU decode kernel");
-  }
+  // pmodel.rs:12.  Not overridden (returns kCanonical): the GPU decoder evaluates
+  // FreqTable::find_index (sample_impl.rs:27-45) itself and decodes ahead.  Overridden:
+  // Decoder::decode calls it at every symbol with the decoder (range_coder(), data() give the
+  // exact state), as decoder.rs:40 does, and param_update uses the index it returns.
+  virtual size_t find_index(const Decoder&) const { return kCanonical; }
+  // An override that keeps FreqTable's binary-search semantics may return true here to keep
+  // the decode-ahead path (its find_index is then not called).
+  virtual bool canonical_find_index() const { return false; }
   // pmodel.rs:14-40
   virtual double ideal_code_length(size_t index) const {
     const double p = (double)c_freq(index);
@@ -268,6 +277,30 @@ inline void throw_flags(uint32_t f, const std::string& where) {
   if (f) throw RangeCoderError(where + ": " + flag_string(f), RC_E_CHUNK, f);
 }
 
+// The reference's error for a BAD_MODEL symbol coded from state (low, range) with (c, cum,
+// total): param_update's own arithmetic (range_coder.rs:53-81, :138-146; u64 products wrap).
+[[noreturn]] inline void throw_bad_model(uint64_t low, uint64_t range, uint32_t c, uint32_t cum,
+                                         uint32_t total, const std::string& where) {
+  RangeCoderError e(where + ": BAD_MODEL", RC_E_CHUNK, RC_F_BAD_MODEL);
+  if (total == 0) {
+    e = RangeCoderError(where + ": range_par_total: attempt to divide by zero", RC_E_CHUNK,
+                        RC_F_BAD_MODEL);
+    e.kind = RangeCoderError::DIVIDE_BY_ZERO;
+    throw e;
+  }
+  const uint64_t r = range / total, nr = r * c, add = r * cum;
+  if (low + add < add) {
+    e = RangeCoderError(where + ": LowerBoundOverflow", RC_E_CHUNK, RC_F_BAD_MODEL);
+    e.kind = RangeCoderError::LOWER_BOUND_OVERFLOW;
+    e.lower_bound = low, e.add_val = add, e.range = nr;
+  } else if (low + add + nr < nr) {
+    e = RangeCoderError(where + ": UpperBoundOverflow", RC_E_CHUNK, RC_F_BAD_MODEL);
+    e.kind = RangeCoderError::UPPER_BOUND_OVERFLOW;
+    e.lower_bound = low + add, e.range = nr;
+  }
+  throw e;
+}
+
 class Encoder;
 
 // Encoder::encode's return value (encoder.rs:34-36: the bytes that symbol settled).  Symbols
@@ -345,10 +378,18 @@ class Encoder {
                                               &len, nb.data(), finish ? 1u : 0u, &fl);
     if (s != RC_OK && s != RC_E_CHUNK) check(s, "rc_stream_encode_host");
     code_.insert(code_.end(), out.begin(), out.begin() + len);
-    counts_.insert(counts_.end(), nb.begin(), nb.begin() + (st_.n - n0));
+    const uint64_t done = st_.n - n0;
+    counts_.insert(counts_.end(), nb.begin(), nb.begin() + done);
     staged0_ += n;
+    const std::string where = "encode (symbol " + std::to_string(st_.n) + ")";
+    if ((fl & RC_F_BAD_MODEL) && done < n) {
+      const uint32_t* t = trip_.data() + 3 * done;
+      const uint32_t c = t[0], cum = t[1], total = t[2];
+      trip_.clear();
+      throw_bad_model(st_.lower_bound, st_.range, c, cum, total, where);
+    }
     trip_.clear();
-    throw_flags(fl, "encode (symbol " + std::to_string(st_.n) + ")");
+    throw_flags(fl, where);
   }
   Context* ctx_;
   rc_stream_state st_ = RC_STREAM_STATE_INIT;
@@ -365,8 +406,8 @@ inline ByteCount::operator uint32_t() const { return e_->count(i_); }
 // binary search and param_update (sample_impl.rs:27-45, decoder.rs:38-54) on the GPU
 // (rc_stream_decode_host).  Symbols are decoded ahead in blocks that double while the table
 // stays the same; when the caller's table changes the state at that symbol is re-derived, so
-// every symbol is decoded with the table held at its call.  The user's find_index is not
-// called (for a table whose (c, cum) intervals tile [0, total) it equals the binary search).
+// every symbol is decoded with the table held at its call.  A PModel that overrides find_index
+// gets it called per symbol and its index decoded (one GPU step per symbol, launch-bound).
 class Decoder {
  public:
   static constexpr uint64_t MAX_BLOCK = 1u << 20;
@@ -385,13 +426,17 @@ class Decoder {
   static Decoder new_(std::vector<uint8_t> code) { return Decoder(std::move(code)); }
 
   size_t decode(const PModel& pm) {  // decoder.rs:38-54
+    if (!pm.canonical_find_index()) {
+      const size_t idx = pm.find_index(*this);  // reads range_coder() / data() at this symbol
+      if (idx != PModel::kCanonical) return decode_index(pm, idx);
+    }
     Table t = table_of(pm);
     const bool same = have_ && t == sig_;
     if (same && bpos_ < buf_.size()) {
       ++taken_;
       return buf_[bpos_++];
     }
-    if (same && err_) throw_flags(err_, "decode (symbol " + std::to_string(taken_) + ")");
+    if (same && err_) decode_error(end_, t, err_);
     block_ = (same && bpos_ == buf_.size()) ? std::min<uint64_t>(2 * block_, MAX_BLOCK) : 1;
     rc_stream_state st = here();
     uint64_t n = block_;
@@ -407,15 +452,15 @@ class Decoder {
     sig_ = std::move(t);
     have_ = true;
     err_ = fl;
-    if (buf_.empty()) throw_flags(fl, "decode (symbol " + std::to_string(taken_) + ")");
+    if (buf_.empty()) decode_error(start, sig_, fl);
     ++taken_;
     return buf_[bpos_++];
   }
-  RangeCoder range_coder() {  // decoder.rs:24-26 (a snapshot)
+  RangeCoder range_coder() const {  // decoder.rs:24-26 (a snapshot)
     const rc_stream_state st = here();
     return RangeCoder(st.lower_bound, st.range);
   }
-  uint64_t data() { return here().data; }  // decoder.rs:27-29
+  uint64_t data() const { return here().data; }  // decoder.rs:27-29
 
  private:
   struct Table {
@@ -423,6 +468,45 @@ class Decoder {
     uint32_t total;
     bool operator==(const Table& o) const { return total == o.total && c == o.c && cum == o.cum; }
   };
+  // decoder.rs:38-54 with the caller's find_index: param_update and shift_left_buffer for the
+  // index it returned, on the GPU (a one-entry table, so the kernel's search has no choice)
+  size_t decode_index(const PModel& pm, size_t idx) {
+    const rc_stream_state st = here();
+    Table t{{pm.c_freq(idx)}, {pm.cum_freq(idx)}, pm.total_freq()};
+    rc_stream_state nxt = st;
+    uint8_t sym = 0;
+    const uint32_t fl = run(nxt, t, 1, &sym);
+    const std::string where = "decode (symbol " + std::to_string(taken_) + ")";
+    if (nxt.n == st.n) {
+      if (fl & RC_F_BAD_MODEL) throw_bad_model(st.lower_bound, st.range, t.c[0], t.cum[0], t.total, where);
+      throw_flags(fl, where);
+    }
+    start_ = end_ = nxt;
+    buf_.clear();
+    bpos_ = 0;
+    have_ = false;
+    err_ = 0;
+    ++taken_;
+    return idx;
+  }
+  // the reference's error for a decode that stopped at state st under table t
+  [[noreturn]] void decode_error(const rc_stream_state& st, const Table& t, uint32_t fl) const {
+    const std::string where = "decode (symbol " + std::to_string(taken_) + ")";
+    if ((fl & RC_F_BAD_MODEL) && t.total && !t.c.empty()) {
+      // the index FreqTable::find_index chose (sample_impl.rs:29-44), for the error's payload
+      const uint64_t rf = (st.data - st.lower_bound) / (st.range / t.total);
+      size_t left = 0, right = t.c.size() - 1;
+      while (left < right) {
+        const size_t mid = (left + right) / 2;
+        if ((uint64_t)t.cum[mid + 1] <= rf) left = mid + 1;
+        else right = mid;
+      }
+      throw_bad_model(st.lower_bound, st.range, t.c[left], t.cum[left], t.total, where);
+    }
+    if (fl & RC_F_BAD_MODEL) throw_bad_model(st.lower_bound, st.range, 0, 0, t.total, where);
+    throw_flags(fl ? fl : RC_F_CORRUPT, where);
+    throw RangeCoderError(where);
+  }
   static Table table_of(const PModel& pm) {
     Table t;
     const size_t n = pm.alphabet_count();
@@ -435,7 +519,7 @@ class Decoder {
     t.total = pm.total_freq();
     return t;
   }
-  uint32_t run(rc_stream_state& st, const Table& t, uint64_t n, uint8_t* out) {
+  uint32_t run(rc_stream_state& st, const Table& t, uint64_t n, uint8_t* out) const {
     uint32_t fl = 0;
     uint8_t dummy = 0;
     const rc_status s = rc_stream_decode_host(ctx_->get(), t.c.data(), t.cum.data(),
@@ -445,7 +529,7 @@ class Decoder {
     return fl;
   }
   // the state at the current symbol (re-derived inside a block, which then starts here)
-  rc_stream_state here() {
+  rc_stream_state here() const {
     if (bpos_ == 0) return start_;
     if (bpos_ == buf_.size()) {
       rc_stream_state st = end_;
@@ -460,11 +544,14 @@ class Decoder {
     bpos_ = 0;
     return st;
   }
+  // (the decode-ahead block is a cache of the stream: range_coder() / data() re-derive into it)
   Context* ctx_;
-  std::vector<uint8_t> code_, buf_;
+  std::vector<uint8_t> code_;
+  mutable std::vector<uint8_t> buf_;
   uint64_t limit_;
-  rc_stream_state start_ = RC_STREAM_STATE_INIT, end_ = RC_STREAM_STATE_INIT;
-  size_t bpos_ = 0;
+  mutable rc_stream_state start_ = RC_STREAM_STATE_INIT;
+  rc_stream_state end_ = RC_STREAM_STATE_INIT;
+  mutable size_t bpos_ = 0;
   Table sig_;
   bool have_ = false;
   uint32_t err_ = 0;

@@ -5,6 +5,7 @@ from .api import (  # noqa: F401
     PModel, RangeCoderError, StaticModel, TruncatedStreamError, ZeroFrequencyError,
     decode_batch, decode_chunks, default_context, encode_batch, encode_chunks, flag_names,
     slot_capacity, encode_host, decode_host, BadModelError, ByteCount, FinishedError, RangeCoder,
+    LowerBoundOverflow, UpperBoundOverflow,
     stream_states, stream_encode_batch, stream_decode_batch, encode_host_multi, decode_host_multi,
 )
 from . import synth  # noqa: F401

@@ -4,12 +4,16 @@ Reference surface (diegodox/range_coder_rust, src/lib.rs:1-13) and what replaces
 
   trait PModel (src/pmodel.rs:4-41)        -> class PModel (same method names/meaning)
   FreqTable example model (sample_impl.rs)  -> class FreqTable
-  Encoder::{new, encode, finish}            -> class Encoder: encode() stages symbols, finish()
-    (src/encoder.rs:14-46)                     encodes the stream on the GPU (one lane)
-  Decoder::{new, decode}                    -> class Decoder(code, n_symbols): the first
-    (src/decoder.rs:14-54)                     decode() decodes the stream on the GPU
+  Encoder::{new, encode, finish, peek_code} -> class Encoder: encode() reads the model at the
+    (src/encoder.rs:14-46)                     call and stages the triple; the resumable stream
+                                               kernel codes staged symbols when a result is needed
+  Decoder::{new, decode, range_coder, data} -> class Decoder(code): decode() reads the model at
+    (src/decoder.rs:14-54)                     the call; symbols are decoded ahead on the GPU while
+                                               the table is unchanged; a PModel with its own
+                                               find_index is called per symbol (see Decoder)
   error::RangeCoderError (src/error.rs)     -> RangeCoderError and subclasses (raised where
-                                               the reference panics or never terminates)
+                                               the reference panics or never terminates), with
+                                               LowerBoundOverflow / UpperBoundOverflow payloads
 
 The hot path proper is the batch API (encode_batch / decode_batch / encode_chunks /
 decode_chunks): many independent chunks per launch, one chunk per GPU lane, through the C ABI
@@ -23,10 +27,13 @@ import numpy as np
 
 from . import _native as N
 
+M64 = (1 << 64) - 1
+
 __all__ = [
     "Context", "StaticModel", "PModel", "FreqTable", "Encoder", "Decoder", "RangeCoderError",
     "ZeroFrequencyError", "BadSymbolError", "TruncatedStreamError", "CorruptStreamError",
     "CapacityError", "ChunkTooLongError", "BadModelError", "FinishedError", "RangeCoder",
+    "LowerBoundOverflow", "UpperBoundOverflow",
     "ByteCount", "encode_host_multi", "decode_host_multi", "stream_states", "stream_encode_batch", "stream_decode_batch", "encode_batch", "decode_batch", "encode_chunks", "decode_chunks",
     "default_context", "flag_names", "slot_capacity",
 ]
@@ -63,6 +70,25 @@ class BadModelError(RangeCoderError):
     (upper_bound().unwrap(), :138-146)."""
 
 
+class LowerBoundOverflow(BadModelError):
+    """RangeCoderError::LowerBoundOverflow (error.rs:5-10): lower_bound + add_val overflowed in
+    param_update (range_coder.rs:68-81).  range is the narrowed range, as the reference reports
+    it (self.range was updated first, :65)."""
+
+    def __init__(self, msg, lower_bound, add_val, range_):
+        super().__init__(msg)
+        self.lower_bound, self.add_val, self.range = lower_bound, add_val, range_
+
+
+class UpperBoundOverflow(BadModelError):
+    """RangeCoderError::UpperBoundOverflow (error.rs:11): lower_bound + range overflowed in
+    upper_bound() (range_coder.rs:138-146), which no_carry_expansion unwraps (a panic)."""
+
+    def __init__(self, msg, lower_bound, range_):
+        super().__init__(msg)
+        self.lower_bound, self.range = lower_bound, range_
+
+
 class FinishedError(RangeCoderError):
     """encode() after finish(): Encoder::finish takes the encoder by value (encoder.rs:40)."""
 
@@ -91,6 +117,27 @@ def _raise_for_flag(f, where):
     for bit, exc in _FLAG_ERRORS:
         if f & bit:
             raise exc(f"{where}: {'|'.join(flag_names(f))}")
+
+
+def _raise_bad_model(low, range_, c, cum, total, where):
+    """The reference's error for a flagged (RC_F_BAD_MODEL) symbol, with its payload.  The stream
+    kernels stop before the failing symbol, so (low, range) is the state param_update started
+    from; the payload is param_update's own arithmetic (range_coder.rs:53-81, :138-146), u64
+    products wrapping as in a release build."""
+    if total == 0:
+        raise BadModelError(f"{where}: range_par_total: attempt to divide by zero")
+    r = range_ // total
+    nr = (r * c) & M64
+    add = (r * cum) & M64
+    if low + add > M64:
+        raise LowerBoundOverflow(
+            f"{where}: Overflow happend while lower_bound uppdating {low} + {add} , {nr}",
+            low, add, nr)
+    nl = low + add
+    if nl + nr > M64:
+        raise UpperBoundOverflow(
+            f"{where}: Overflow happend when calc upper_bound {nl} + {nr}", nl, nr)
+    raise BadModelError(f"{where}: BAD_MODEL")
 
 
 # ----------------------------------------------------------------------------- torch glue
@@ -177,7 +224,13 @@ class PModel:
     def total_freq(self):  # pmodel.rs:10
         raise NotImplementedError
 
-    def find_index(self, decoder):  # pmodel.rs:12 — not called by the GPU path (see StaticModel)
+    def find_index(self, decoder):  # pmodel.rs:12
+        """Not overridden: the decoder runs FreqTable::find_index (sample_impl.rs:27-45) itself,
+        on the GPU.  Override it to decode with your own rule: Decoder.decode then calls it at
+        every symbol with the decoder (range_coder() / data()), as decoder.rs:40 does, and
+        applies param_update to the index it returns.  A subclass that overrides it but keeps
+        FreqTable's binary-search semantics can set canonical_find_index = True to keep the
+        decode-ahead path."""
         raise NotImplementedError
 
     def ideal_code_length(self, index):  # pmodel.rs:14-40
@@ -462,7 +515,6 @@ def decode_chunks(model, codes, counts, raise_on_error=True):
 
 
 # ----------------------------------------------------------------------------- stream API
-M64 = (1 << 64) - 1
 
 
 class RangeCoder:
@@ -546,10 +598,30 @@ class ByteCount:
     def __hash__(self):
         return hash(int(self))
 
+    def __bool__(self):
+        return int(self) != 0
+
+    def __float__(self):
+        return float(int(self))
+
     def __add__(self, other):
         return int(self) + other
 
     __radd__ = __add__
+
+    def __sub__(self, other):
+        return int(self) - other
+
+    def __rsub__(self, other):
+        return other - int(self)
+
+    def __mul__(self, other):
+        return int(self) * other
+
+    __rmul__ = __mul__
+
+    def __floordiv__(self, other):
+        return int(self) // other
 
     def __repr__(self):
         return repr(int(self))
@@ -560,6 +632,40 @@ def _u32(v, what):
     if not 0 <= v <= 0xFFFFFFFF:
         raise RangeCoderError(f"{what} = {v} is not a u32")
     return v
+
+
+def _canonical_find_index(pmodel):
+    """True when decoding may use FreqTable::find_index's binary search (sample_impl.rs:27-45):
+    the model does not override find_index (pmodel.rs:12), or says its override has those
+    semantics (canonical_find_index = True in the class that defines the override)."""
+    owner = next((k for k in type(pmodel).__mro__ if "find_index" in vars(k)), None)
+    if owner is None or owner is PModel or owner is FreqTable:
+        return True
+    return bool(vars(owner).get("canonical_find_index", False))
+
+
+def _find_index_rfreq(st, total):
+    """rfreq of FreqTable::find_index (sample_impl.rs:29): (data - lower_bound) / range_par_total.
+    Only for error reports (the decode itself ran on the GPU)."""
+    return ((st.data - st.lower_bound) & M64) // (st.range // total)
+
+
+def _decode_error(st, sig, flags, where):
+    """Raise the reference's error for a decode that stopped at state st under table sig."""
+    if flags & N.F_BAD_MODEL:
+        c, cum, total = sig
+        if total == 0 or not c:
+            raise BadModelError(f"{where}: range_par_total: attempt to divide by zero")
+        rf = _find_index_rfreq(st, total)
+        left, right = 0, len(c) - 1  # the binary search of sample_impl.rs:31-44
+        while left < right:
+            mid = (left + right) // 2
+            if cum[mid + 1] <= rf:
+                left = mid + 1
+            else:
+                right = mid
+        _raise_bad_model(st.lower_bound, st.range, c[left], cum[left], total, where)
+    _raise_for_flag(flags, where)
 
 
 def _table_of(pmodel):
@@ -594,6 +700,7 @@ class Encoder:
         self._counts = bytearray()  # encode() return values of the flushed symbols
         self._staged0 = 0          # index of the first staged symbol
         self._finished = False
+        self._exc = None           # the error of the failing symbol, raised again after it
 
     @classmethod
     def new(cls):  # encoder.rs:14-16
@@ -642,7 +749,9 @@ class Encoder:
         n = len(self._trip) // 3
         if n == 0 and not finish:
             return
-        if self._state.flags:
+        if self._state.flags:  # the reference panicked at an earlier call
+            if self._exc is not None:
+                raise self._exc
             _raise_for_flag(self._state.flags, "encode")
         ctx = self._ctx or default_context()
         trip = np.array(self._trip, dtype=np.uint32)
@@ -658,11 +767,20 @@ class Encoder:
         if rc not in (N.RC_OK, N.RC_E_CHUNK):
             N.check(rc, "rc_stream_encode_host")
         self._code += out[: out_len.value].tobytes()
-        self._counts += nb[: self._state.n - n0].tobytes()
+        done = self._state.n - n0
+        self._counts += nb[:done].tobytes()
+        failed = self._trip[3 * done: 3 * done + 3]
         self._staged0 += n
         self._trip = []
         if fl.value:
-            _raise_for_flag(fl.value, f"encode (symbol {self._state.n})")
+            where = f"encode (symbol {self._state.n})"
+            try:
+                if fl.value & N.F_BAD_MODEL and len(failed) == 3:
+                    _raise_bad_model(self._state.lower_bound, self._state.range, *failed, where)
+                _raise_for_flag(fl.value, where)
+            except RangeCoderError as e:
+                self._exc = e
+                raise
 
 
 class Decoder:
@@ -675,9 +793,14 @@ class Decoder:
     resumable stream kernel.  Symbols are decoded ahead in blocks that double while the table
     stays the same; when the caller's table changes (an adaptive PModel), the state at that
     symbol is re-derived and decoding continues under the new table, so every symbol is decoded
-    with the table the caller held at its call.  The user's find_index is not called: for a
-    PModel whose (c, cum) intervals tile [0, total) — the contract decoding relies on — it
-    returns what the binary search returns.  n_symbols (optional, out-of-band as in
+    with the table the caller held at its call.
+
+    A PModel that overrides find_index (pmodel.rs:12) gets it called, as decoder.rs:40 does:
+    once per symbol, with this decoder (range_coder(), data() give the exact state), and the
+    index it returns is what param_update uses (one GPU step per symbol, with the table cut to
+    that index's (c_freq, cum_freq)).  That path is launch-latency-bound; a subclass whose
+    override keeps FreqTable's binary-search semantics can set canonical_find_index = True to
+    stay on the decode-ahead path.  n_symbols (optional, out-of-band as in
     sample_impl.rs:113-120) only bounds the decode-ahead."""
 
     MAX_BLOCK = 1 << 20
@@ -742,6 +865,8 @@ class Decoder:
         return st
 
     def decode(self, pmodel):  # decoder.rs:38-54
+        if not _canonical_find_index(pmodel):
+            return self._decode_by_find_index(pmodel)
         sig = _table_of(pmodel)
         if sig == self._sig and self._bpos < len(self._buf):
             s = self._buf[self._bpos]
@@ -749,7 +874,7 @@ class Decoder:
             self._taken += 1
             return int(s)
         if sig == self._sig and self._err:  # the reference panics / hangs at this symbol
-            _raise_for_flag(self._err, f"decode (symbol {self._taken})")
+            _decode_error(self._end, sig, self._err, f"decode (symbol {self._taken})")
         if sig == self._sig and self._bpos == len(self._buf):
             self._block = min(2 * self._block, self.MAX_BLOCK)
         else:
@@ -763,10 +888,31 @@ class Decoder:
         self._start, self._end, self._buf, self._bpos = start, st, syms, 0
         self._sig, self._err = sig, fl
         if len(syms) == 0:
-            _raise_for_flag(fl, f"decode (symbol {self._taken})")
+            _decode_error(st, sig, fl, f"decode (symbol {self._taken})")
         self._bpos = 1
         self._taken += 1
         return int(syms[0])
+
+    def _decode_by_find_index(self, pmodel):
+        """decoder.rs:38-54 with the caller's find_index: the index it returns at this state,
+        then param_update and shift_left_buffer on the GPU (a one-entry table (c, cum) of that
+        index, so the kernel's search has nothing to choose)."""
+        st = self._copy(self._here())
+        self._start, self._end, self._bpos = st, st, 0
+        self._buf, self._sig, self._err = np.zeros(0, np.uint8), None, 0
+        idx = int(pmodel.find_index(self))  # reads range_coder() / data(): the state st
+        where = f"decode (symbol {self._taken})"
+        sig = ((_u32(pmodel.c_freq(idx), "c_freq"),), (_u32(pmodel.cum_freq(idx), "cum_freq"),),
+               _u32(pmodel.total_freq(), "total_freq"))
+        nxt = self._copy(st)
+        syms, fl = self._run(nxt, sig, 1)
+        if len(syms) == 0:
+            if fl & N.F_BAD_MODEL:
+                _raise_bad_model(st.lower_bound, st.range, sig[0][0], sig[1][0], sig[2], where)
+            _raise_for_flag(fl, where)
+        self._start = self._end = nxt
+        self._taken += 1
+        return idx
 
     def range_coder(self):  # decoder.rs:24-26 (a snapshot)
         st = self._here()

@@ -27,6 +27,22 @@ typedef u32 u32x3 __attribute__((ext_vector_type(3)));
 #define RC_VGPR_FLOOR_144() asm volatile("; vgpr floor 144" ::: "v143")
 #define RC_VGPR_FLOOR_160() asm volatile("; vgpr floor 160" ::: "v159")
 
+// Scratch builds only ("what binds"): -DRC_FILL=n adds n independent 2-cycle
+// VALU instructions to every symbol step of the static coders.  If the step is bound by VALU
+// issue the kernel slows by about n x 2 cycles per wave-symbol; if it waits on latency, the
+// fillers ride in idle issue slots.
+#ifdef RC_FILL
+#define RC_FILLER(x)                                                   \
+  do {                                                                 \
+    _Pragma("unroll") for (int i_ = 0; i_ < RC_FILL; ++i_)             \
+        asm volatile("v_add_u32 %0, 1, %0" : "+v"(x));                 \
+  } while (0)
+#else
+#define RC_FILLER(x) \
+  do {               \
+  } while (0)
+#endif
+
 static __device__ __forceinline__ u32 hi32(u64 v) { return (u32)(v >> 32); }
 
 // a - b (64-bit) with the borrow in an SGPR pair: the compiler's v_subb_co_u32_e32 reads VCC,

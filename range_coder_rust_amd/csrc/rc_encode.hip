@@ -24,6 +24,9 @@ struct Enc {
   u32 B;           // bit position of the next settled byte, from the 64-B aligned slot base:
                    // dword B >> 5 of the stream is the incomplete one (its ring slot is free)
   u32 fpos;        // byte position of the next unit to store
+#ifdef RC_FILL
+  u32 fill;        // scratch builds: the filler instructions' register
+#endif
   u32 err;         // first RC_F_* error of this chunk (SM: OR of staged table flags)
   u32 ring;        // LDS byte address of this lane's ring column: dword j at ring + 256 * j.
                    // The ring holds stream dwords as values (first byte in the top bits);
@@ -121,6 +124,9 @@ static __device__ __forceinline__ void enc_rare(Enc& e) {
 // cannot encode; 2 small and complete (256 symbols, every c > 0: nothing to check)
 template <int DIV, int SM>
 static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint2 t) {
+#ifdef RC_FILL
+  RC_FILLER(e.fill);
+#endif
   u32 c, cum;
   if (SM == 2) {
     cum = t.x;
@@ -282,6 +288,9 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   const EncOut* wout = s_out + wave * 64;
 
   Enc e;
+#ifdef RC_FILL
+  e.fill = 0;
+#endif
   e.low = 0;  // RangeCoder::default (range_coder.rs:13-20)
   e.range = ~0ull;
   e.acc = 0;

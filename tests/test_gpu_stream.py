@@ -331,3 +331,158 @@ def test_cpp_caller_adaptive_model(ctx):
     assert r.returncode == 0, r.stdout + r.stderr
     want = R.encode_adaptive_stream(256, 32, 4000, 64, _xorshift_syms(n, seed))
     assert r.stdout.strip() == want.hex()
+
+
+def _canonical_index(c, cum, total, low, rng, data):
+    """FreqTable::find_index (sample_impl.rs:27-45), for the test models below."""
+    rf = ((data - low) & ((1 << 64) - 1)) // (rng // total)
+    left, right = 0, len(c) - 1
+    while left < right:
+        mid = (left + right) // 2
+        if cum[mid + 1] <= rf:
+            left = mid + 1
+        else:
+            right = mid
+    return left
+
+
+class _Linear(rc.FreqTable):
+    """find_index overridden by a linear scan (same inverse as the binary search)."""
+    calls = 0
+
+    def find_index(self, decoder):
+        type(self).calls += 1
+        r = decoder.range_coder()
+        rf = ((decoder.data() - r.lower_bound()) & ((1 << 64) - 1)) // (r.range() // self.total)
+        i = 0
+        while i + 1 < len(self.c) and self.cum[i + 1] <= rf:
+            i += 1
+        return i
+
+
+class _NextUp(rc.FreqTable):
+    """A different inverse: the canonical symbol's successor where that has c > 0."""
+
+    def find_index(self, decoder):
+        r = decoder.range_coder()
+        i = _canonical_index(self.c, self.cum, self.total, r.lower_bound(), r.range(),
+                             decoder.data())
+        return i + 1 if i + 1 < len(self.c) and self.c[i + 1] else i
+
+
+class _RefNextUp(R.FreqTable):
+    def find_index(self, decoder):
+        rcd = decoder.range_coder
+        i = _canonical_index(self.c, self.cum, self.total, rcd.lower_bound, rcd.range,
+                             decoder.data)
+        return i + 1 if i + 1 < len(self.c) and self.c[i + 1] else i
+
+
+class _Opted(_Linear):
+    canonical_find_index = True  # the override keeps the binary search's semantics
+
+
+def test_custom_find_index_is_called(ctx):
+    """pmodel.rs:12 / decoder.rs:40: a model's own find_index decides every decoded index."""
+    sd = _sample_table()
+    enc = rc.Encoder()
+    for i in SAMPLE:
+        enc.encode(sd, i)
+    code = enc.finish()
+    lin = _Linear(10)
+    lin.c = list(sd.c)
+    lin.calc_cum()
+    _Linear.calls = 0
+    dec = rc.Decoder(code)
+    assert [dec.decode(lin) for _ in SAMPLE] == SAMPLE
+    assert _Linear.calls == len(SAMPLE)
+    # opted in: the decode-ahead path, find_index never called
+    opt = _Opted(10)
+    opt.c = list(sd.c)
+    opt.calc_cum()
+    _Linear.calls = 0
+    dec = rc.Decoder(code)
+    assert [dec.decode(opt) for _ in SAMPLE] == SAMPLE and _Linear.calls == 0
+
+
+def test_custom_find_index_other_inverse_vs_reference(ctx):
+    """A find_index with a different inverse decodes other symbols: exactly the reference's,
+    symbol by symbol, until the reference panics (then the same error class at that call)."""
+    rng = random.Random(11)
+    counts = [rng.randint(1, 40) for _ in range(32)]
+    syms = [rng.randrange(32) for _ in range(300)]
+    m = rc.FreqTable.from_counts(counts)
+    enc = rc.Encoder()
+    for s in syms:
+        enc.encode(m, s)
+    code = enc.finish()
+    ours = _NextUp(32)
+    ours.c = list(counts)
+    ours.calc_cum()
+    ref_m = _RefNextUp.from_counts(counts)
+    ref = R.Decoder(code)
+    dec = rc.Decoder(code)
+    got, want, ref_err = [], [], None
+    for _ in range(len(syms)):
+        try:
+            want.append(ref.decode(ref_m))
+        except (R.ReferencePanic, R.RangeCoderError) as e:
+            ref_err = e
+            break
+        got.append(dec.decode(ours))
+    assert got == want and want != syms[:len(want)]
+    if ref_err is not None:
+        with pytest.raises(rc.RangeCoderError):
+            dec.decode(ours)
+
+
+def test_lower_bound_overflow_payload(ctx):
+    """error.rs:5-10: LowerBoundOverflow {lower_bound, add_val, range} at the failing encode."""
+    class Bad(rc.PModel):
+        def __init__(self):
+            self.bad = False
+
+        def alphabet_count(self):
+            return 2
+
+        def c_freq(self, i):
+            return 1
+
+        def cum_freq(self, i):
+            return 0xFFFFFFFF if self.bad else i
+
+        def total_freq(self):
+            return 2
+
+    m = Bad()
+    enc = rc.Encoder()
+    ref = R.Encoder()
+    for i in (1, 1, 0, 1):  # a lower bound well above 0
+        enc.encode(m, i)
+        ref.encode(m, i)
+    m.bad = True
+    low, rng_ = ref.range_coder.lower_bound, ref.range_coder.range
+    r = rng_ // 2
+    add, nr = (r * 0xFFFFFFFF) & ((1 << 64) - 1), r
+    assert low + add > (1 << 64) - 1  # the reference's overflowing_add fails here
+    enc.encode(m, 1)
+    with pytest.raises(rc.LowerBoundOverflow) as ei:
+        enc.peek_code()
+    e = ei.value
+    assert (e.lower_bound, e.add_val, e.range) == (low, add, nr)
+    with pytest.raises(rc.LowerBoundOverflow):  # the encoder stays failed, as after a panic
+        enc.peek_code()
+
+
+def test_cpp_find_index(ctx):
+    """examples/find_index_impl.cpp: an overridden find_index is called per symbol, and
+    LowerBoundOverflow carries the reference's payload, through the C++ host API."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples",
+                       "find_index_impl")
+    if not os.path.exists(exe):
+        pytest.skip("examples/find_index_impl not built")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "find_index called 16 times" in r.stdout and "test passed" in r.stdout
