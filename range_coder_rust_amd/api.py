@@ -746,13 +746,13 @@ class Encoder:
         return self._counts[i]
 
     def _flush(self, finish=False):
-        n = len(self._trip) // 3
-        if n == 0 and not finish:
-            return
         if self._state.flags:  # the reference panicked at an earlier call
             if self._exc is not None:
                 raise self._exc
             _raise_for_flag(self._state.flags, "encode")
+        n = len(self._trip) // 3
+        if n == 0 and not finish:
+            return
         ctx = self._ctx or default_context()
         trip = np.array(self._trip, dtype=np.uint32)
         cap = N.stream_max_bytes(n, finish)
