@@ -320,20 +320,62 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
       lut.swap(wide);
     }
   }
+  // pair buckets (k_decode_static LUT 3, rc_static.h): 2^15 < total <= 2^16, so buckets of 16
+  // frequencies, and every c < 2^16 (16-bit fields).  Per bucket both candidates of its bucket
+  // entry: s0 (holding the bucket's first frequency) and s1 (the next symbol with c > 0 that
+  // starts inside the bucket; none: s1 = s0, so the choice between them does not matter).
+  std::vector<u32> pair;
+  u32 cmax = 0;
+  for (u32 i = 0; i < n_symbols; ++i) cmax = std::max(cmax, c_freq[i]);
+  if (!a.direct && total_freq > 32768 && total_freq <= 65536 && cmax < 65536) {
+    pair.assign(PAIR_WORDS, 0);
+    uint16_t* sp = (uint16_t*)pair.data();
+    u32* ent = pair.data() + PAIR_S_WORDS;
+    auto tcb = [&](u32 sym) {
+      const float tcf = c_freq[sym] ? (float)total_freq / (float)c_freq[sym] : 0.0f;
+      u32 b;
+      memcpy(&b, &tcf, 4);
+      return b;
+    };
+    for (u32 b = 0; b < PAIR_BUCKETS; ++b) {
+      const u32 e = lut[b];  // the bucket entry built above (padded buckets repeat the last)
+      const u32 s0 = e & 255u, s1 = (e >> 8) & 255u;  // (s1 = s0 where there is no split)
+      sp[b] = (uint16_t)(s0 | s1 << 8);
+      ent[4 * b + 0] = cum_freq[s0] | c_freq[s0] << 16;
+      ent[4 * b + 1] = cum_freq[s1] | c_freq[s1] << 16;
+      ent[4 * b + 2] = tcb(s0);
+      ent[4 * b + 3] = tcb(s1);
+    }
+  }
+  // small bucket models (the decoder's SM path) test the hint against s1's absolute cum, one
+  // instruction fewer than its offset inside the bucket
+  if (!a.direct && total_freq <= 65536) {
+    for (size_t b = 0; b < lut.size(); ++b) {
+      const u32 e = lut[b], split = e >> 16;
+      // (padded buckets repeat the last real one, (total - 1) >> lut_shift)
+      const u32 br = (u32)std::min<size_t>(b, (total_freq - 1) >> a.lut_shift);
+      const u32 cum1 = split == 0xFFFFu ? 0u : (br << a.lut_shift) + split;
+      lut[b] = (e & 0xFFFFu) | cum1 << 16;
+    }
+  }
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
   const size_t tab_bytes = 256 * sizeof(uint2);
   const size_t lut_bytes = lut.size() * sizeof(u32);
+  const size_t pair_bytes = pair.size() * sizeof(u32);
   void* d = nullptr;
-  if (hipMalloc(&d, tab_bytes + lut_bytes) != hipSuccess) return RC_E_DEVICE;
+  if (hipMalloc(&d, tab_bytes + lut_bytes + pair_bytes) != hipSuccess) return RC_E_DEVICE;
   if (hipMemcpy(d, tab.data(), tab_bytes, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy((char*)d + tab_bytes, lut.data(), lut_bytes, hipMemcpyHostToDevice) !=
-          hipSuccess) {
+          hipSuccess ||
+      (pair_bytes && hipMemcpy((char*)d + tab_bytes + lut_bytes, pair.data(), pair_bytes,
+                               hipMemcpyHostToDevice) != hipSuccess)) {
     (void)hipFree(d);
     return RC_E_DEVICE;
   }
   a.tab = (const uint2*)d;
   a.lut = (const u32*)((char*)d + tab_bytes);
+  a.pair = pair_bytes ? (const u32*)((char*)d + tab_bytes + lut_bytes) : nullptr;
   rc_model* mm = new rc_model;
   mm->kind = 0;
   mm->device = ctx->device;

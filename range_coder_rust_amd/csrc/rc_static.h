@@ -41,6 +41,9 @@
 #ifndef DEC_OUT_BURST
 #define DEC_OUT_BURST 4      // 16-B symbol blocks per lane per output burst (4: 64 B)
 #endif
+#ifndef DEC_SPEC
+#define DEC_SPEC 1           // every SM decoder takes the speculative step (verify deferred)
+#endif
 #ifndef DEC_TAB_LDS
 #define DEC_TAB_LDS 1        // direct-LUT decoders: keep the (cum, c) table in LDS too
 #endif
@@ -51,7 +54,8 @@ enum { DIV_POW2 = 0, DIV_MAGIC = 1 };
 
 struct ModelArgs {
   const uint2* tab;  // [256] (cum, c); entries s >= n_symbols hold (0xFFFFFFFF, 0)
-  const u32* lut;    // decoder buckets: s0 | s1 << 8 | split << 16
+  const u32* lut;    // decoder buckets: s0 | s1 << 8 | split << 16 (small models, total <=
+                     // 2^16: s0 | s1 << 8 | cum[s1] << 16, and s1 = s0 without a split)
   u64 magic;         // floor((2^64 - 1) / total) for DIV_MAGIC
   u32 n;             // alphabet size (1..256)
   u32 total;         // total_freq
@@ -61,7 +65,19 @@ struct ModelArgs {
   float ftotal;      // (float)total
   u32 direct;        // 1: lut[q] = s | cum << 8 | c << 20 for every q < total (total <= 2048)
                      // 2: lut[4q..4q+3] = {cum, c, s, total/c as f32} (256 <= total <= 512)
+  const u32* pair;   // pair-bucket tables (k_decode_static LUT 3; null when the model has none):
+                     // PAIR_S_WORDS words of {s0 | s1 << 8} (u16 per bucket), then one 16-B
+                     // entry per bucket {cum0 | c0 << 16, cum1 | c1 << 16, total/c0, total/c1}
 };
+
+// Pair-bucket decoding (LUT 3): models with 2^15 < total <= 2^16 (buckets of 16 frequencies) and
+// every c < 2^16.  A bucket's entry holds both candidates of its bucket table entry, so the
+// symbol step reads LDS once (the bucket decoder reads the bucket, then the candidate's table
+// entry).  The u16 symbol pairs come first in LDS, the entries at PAIR_ENT_OFF.
+#define PAIR_BUCKETS 4096u
+#define PAIR_S_WORDS (PAIR_BUCKETS / 2)
+#define PAIR_ENT_OFF (PAIR_S_WORDS * 4)            // bytes
+#define PAIR_WORDS (PAIR_S_WORDS + 4 * PAIR_BUCKETS)
 
 
 // RangeCoder::range_par_total (range_coder.rs:38-40): range / total, exact.
@@ -91,6 +107,19 @@ static __device__ __forceinline__ u64 mul_rv(u64 r, u32 v) {
 }
 
 
+// r * v + a (mod 2^64): the same two instructions with the 64-bit addend folded into the first
+template <int SM>
+static __device__ __forceinline__ u64 mad_rv(u64 r, u32 v, u64 a) {
+  if (SM) {
+    u64 p, c;
+    u32 h;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(p), "=s"(c) : "v"((u32)r), "v"(v), "v"(a));
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(r)), "v"(v), "v"(hi32(p)));
+    return ((u64)h << 32) | (u32)p;
+  }
+  return r * (u64)v + a;
+}
+
 // v_ffbh_u32 as the hardware defines it: 0xFFFFFFFF for 0 (the clz builtins are undefined there)
 static __device__ __forceinline__ u32 ffbh(u32 v) {
   u32 r;
@@ -102,8 +131,9 @@ static __device__ __forceinline__ u32 ffbh(u32 v) {
 hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a, int div, int smv,
                                    const uint8_t* syms, const u64* sym_off, u32 n_chunks,
                                    uint8_t* out, const u64* out_off, u64* out_len, u32* flags);
-// dynamic LDS bytes of k_decode_static for a model
-size_t rc_static_decode_lds(const ModelArgs& a);
+// dynamic LDS bytes of k_decode_static for a model (lut3: the pair-bucket variant, wgs lanes
+// per workgroup)
+size_t rc_static_decode_lds(const ModelArgs& a, int lut3, u32 wgs);
 hipError_t rc_static_decode_launch_pow2(hipStream_t stream, const ModelArgs& a, int sm,
                                         const uint8_t* code, const u64* code_off,
                                         const u64* code_len, uint8_t* syms_out,

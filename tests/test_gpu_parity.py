@@ -396,3 +396,54 @@ def test_cpp_sample_impl(ctx):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "output : 0x64475f8970365a2f83b20246c0" in r.stdout
     assert "test passed" in r.stdout
+
+
+def _pair_models(rng):
+    """Models of the pair-bucket decoder (2^15 < total <= 2^16): Zipf, skewed with zero
+    frequencies and c = 1 runs (buckets with several symbol starts: the exact fix-up), and the
+    extreme totals."""
+    zc, _, zt = synth.zipf_table()
+    out = [(zc.astype(np.uint32), zt)]
+    for total in (32769, 40000, 65535, 65536):
+        n = int(rng.choice([2, 3, 50, 200, 256]))
+        w = rng.pareto(1.0, n) + 0.01
+        c = np.floor(w / w.sum() * total).astype(np.int64)
+        if n > 3:
+            c[rng.random(n) < 0.2] = 0
+            c[rng.choice(n, min(10, n), replace=False)] = 1
+        c[int(np.argmax(c))] += total - int(c.sum())
+        if c.max() >= 65536:  # one symbol holding everything: no pair table (16-bit fields)
+            c[0] -= 1
+            c[1] += 1
+        out.append((c.astype(np.uint32), total))
+    return out
+
+
+@pytest.mark.parametrize("pair", ["512", "1024", "0"])
+def test_pair_bucket_decoder_vs_oracle(ctx, monkeypatch, pair):
+    """k_decode_static LUT 3 (both candidates of a bucket in one 16-B LDS entry) at both
+    workgroup sizes, and the bucket decoder it replaces at low occupancy (RC_DEC_PAIR=0), on the
+    same streams: decoded symbols against the oracle's, ragged and misaligned chunks; garbage
+    streams decode like the reference's find_index, flags included."""
+    monkeypatch.setenv("RC_DEC_PAIR", pair)
+    rng = np.random.default_rng(77)
+    for mi, (c, total) in enumerate(_pair_models(rng)):
+        cum = cum_of(c)
+        m = rc.StaticModel(c, cum, total)
+        nz = np.nonzero(c)[0]
+        p = c[nz] / c[nz].sum()
+        lens = list(rng.choice([0, 1, 15, 16, 17, 64, 65, 257, 1000, 4099], 96))
+        chunks = [rng.choice(nz, L, p=p).astype(np.uint8) for L in lens]
+        codes = [cpu.encode(c, cum, total, ch)[1] for ch in chunks]
+        dec, fd = run_decode(m, codes, lens, misalign=(mi % 2 == 0), seed=mi)
+        for k, ch in enumerate(chunks):
+            assert fd[k] == 0 and (dec[k] == ch).all(), (mi, k)
+        garbage = [rng.integers(0, 256, int(rng.integers(8, 400))).astype(np.uint8).tobytes()
+                   for _ in range(64)]
+        counts = [int(rng.integers(0, 300)) for _ in garbage]
+        dec, fd = run_decode(m, garbage, counts, misalign=True, seed=mi + 100)
+        for k in range(len(garbage)):
+            f, d = cpu.decode(c, cum, total, garbage[k], counts[k])
+            assert fd[k] == f, (mi, k, fd[k], f)
+            if f == 0:
+                assert (dec[k] == d).all(), (mi, k)
