@@ -264,35 +264,41 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
   const bool pow2 = (total_freq & (total_freq - 1)) == 0;
   a.lg = pow2 ? (u32)__builtin_ctz(total_freq) : 0u;
   a.magic = ~0ull / (u64)total_freq;
+  // bucket table of 2^bits buckets: s0 = symbol containing the bucket's first frequency, s1 =
+  // the next symbol with c > 0 starting inside the bucket, split = its offset (0xFFFF: none);
+  // padded to a power of two (the kernel masks the bucket index) with the last bucket, so
+  // exactly 2^bits entries whenever total > 2048
   const u32 bl = bitlen(total_freq - 1);
-  a.lut_shift = bl > LUT_BITS ? bl - LUT_BITS : 0u;
-  a.lut_max = (total_freq - 1) >> a.lut_shift;
-  // bucket table: s0 = symbol containing the bucket's first frequency, s1 = the next symbol
-  // with c > 0 starting inside the bucket, split = its offset (0xFFFF: none)
-  std::vector<u32> lut(a.lut_max + 1);
-  u32 s = 0;
-  for (u32 b = 0; b <= a.lut_max; ++b) {
-    const u64 f0 = (u64)b << a.lut_shift;
-    const u64 f1 = std::min<u64>((u64)(b + 1) << a.lut_shift, total_freq);
-    while (s + 1 < n_symbols && (u64)cum_freq[s + 1] <= f0) ++s;
-    u32 s1 = s, split = 0xFFFFu;
-    for (u32 t = s + 1; t < n_symbols; ++t) {
-      if ((u64)cum_freq[t] >= f1) break;
-      if (c_freq[t] > 0) {
-        if ((u64)cum_freq[t] - f0 <= 0xFFFFu) {
-          s1 = t;
-          split = (u32)((u64)cum_freq[t] - f0);
+  auto bucket_lut = [&](u32 bits, u32* shift_out) {
+    const u32 shift = bl > bits ? bl - bits : 0u;
+    const u32 nb = ((total_freq - 1) >> shift) + 1;
+    std::vector<u32> lt(nb);
+    u32 s = 0;
+    for (u32 b = 0; b < nb; ++b) {
+      const u64 f0 = (u64)b << shift;
+      const u64 f1 = std::min<u64>((u64)(b + 1) << shift, total_freq);
+      while (s + 1 < n_symbols && (u64)cum_freq[s + 1] <= f0) ++s;
+      u32 s1 = s, split = 0xFFFFu;
+      for (u32 t = s + 1; t < n_symbols; ++t) {
+        if ((u64)cum_freq[t] >= f1) break;
+        if (c_freq[t] > 0) {
+          if ((u64)cum_freq[t] - f0 <= 0xFFFFu) {
+            s1 = t;
+            split = (u32)((u64)cum_freq[t] - f0);
+          }
+          break;
         }
-        break;
       }
+      lt[b] = s | (s1 << 8) | (split << 16);
     }
-    lut[b] = s | (s1 << 8) | (split << 16);
-  }
-  // pad to a power of two (the kernel masks the bucket index) with the last bucket: 2^LUT_BITS
-  // entries whenever total > 2048 (the decoder extracts LUT_BITS bits of the hint)
-  while (lut.size() & (lut.size() - 1)) lut.push_back(lut.back());
+    while (lt.size() & (lt.size() - 1)) lt.push_back(lt.back());
+    *shift_out = shift;
+    return lt;
+  };
+  a.lut_bits = total_freq <= 65536 ? SM_LUT_BITS : LUT_BITS;
+  std::vector<u32> lut = bucket_lut(a.lut_bits, &a.lut_shift);
   a.lut_max = (u32)lut.size() - 1;
-  if (total_freq > 2048 && lut.size() != LUT_MAX_ENTRIES) return RC_E_BAD_MODEL;  // unreachable
+  if (total_freq > 2048 && lut.size() != (1u << a.lut_bits)) return RC_E_BAD_MODEL;  // unreachable
 
   if (total_freq <= 2048) {  // direct table: q -> s | cum << 8 | c << 20
     a.direct = 1;
@@ -337,8 +343,11 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
       memcpy(&b, &tcf, 4);
       return b;
     };
+    u32 pshift = 0;
+    const std::vector<u32> plut = bucket_lut(LUT_BITS, &pshift);  // 2^12 buckets of 16
+    if (pshift != 4 || plut.size() != PAIR_BUCKETS) return RC_E_BAD_MODEL;  // unreachable
     for (u32 b = 0; b < PAIR_BUCKETS; ++b) {
-      const u32 e = lut[b];  // the bucket entry built above (padded buckets repeat the last)
+      const u32 e = plut[b];  // (padded buckets repeat the last)
       const u32 s0 = e & 255u, s1 = (e >> 8) & 255u;  // (s1 = s0 where there is no split)
       sp[b] = (uint16_t)(s0 | s1 << 8);
       ent[4 * b + 0] = cum_freq[s0] | c_freq[s0] << 16;

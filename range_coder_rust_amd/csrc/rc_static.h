@@ -49,6 +49,12 @@
 #endif
 #define LUT_BITS 12
 #define LUT_MAX_ENTRIES (1u << LUT_BITS)
+#ifndef SM_LUT_BITS
+// buckets of small models (total <= 2^16).  11 bits would keep LUT + table + rings of a
+// 256-lane workgroup at 30 KiB, 5 workgroups (5 waves per SIMD) per CU instead of 4; measured
+// within 0.5% at 2^20 chunks (3.2 rounds of resident lanes instead of 4)
+#define SM_LUT_BITS 12
+#endif
 
 enum { DIV_POW2 = 0, DIV_MAGIC = 1 };
 
@@ -62,6 +68,7 @@ struct ModelArgs {
   u32 lg;            // log2(total) for DIV_POW2
   u32 lut_shift;     // bucket = q >> lut_shift
   u32 lut_max;       // number of buckets - 1
+  u32 lut_bits;      // bucket tables: log2(buckets) (LUT_BITS, or SM_LUT_BITS for small models)
   float ftotal;      // (float)total
   u32 direct;        // 1: lut[q] = s | cum << 8 | c << 20 for every q < total (total <= 2048)
                      // 2: lut[4q..4q+3] = {cum, c, s, total/c as f32} (256 <= total <= 512)
