@@ -43,9 +43,11 @@ def parse(text):
     return ins
 
 
-def hot_loop(ins):
+def hot_loop(ins, min_steps=64):
+    """The shortest loop closed by a conditional backward branch that holds at least min_steps
+    symbol steps (v_ffbh_u32, one per step); else the longest such loop."""
     idx = {a: i for i, (a, _) in enumerate(ins)}
-    best = None
+    loops = []
     for i, (a, t) in enumerate(ins):
         m = re.match(r"(s_cbranch_\w+)\s+(-?\d+)", t)
         if not m:
@@ -53,9 +55,12 @@ def hot_loop(ins):
         v = int(m.group(2))
         v = v - 65536 if v > 32767 else v
         tgt = a + 4 + 4 * v
-        if tgt <= a and tgt in idx and (best is None or i - idx[tgt] > best[1] - best[0]):
-            best = (idx[tgt], i)
-    return ins[best[0]:best[1] + 1]
+        if tgt <= a and tgt in idx:
+            loops.append((idx[tgt], i))
+    steps = [(j, i) for j, i in loops
+             if sum(t.startswith("v_ffbh") for _, t in ins[j:i + 1]) >= min_steps]
+    j, i = min(steps, key=lambda x: x[1] - x[0]) if steps else max(loops, key=lambda x: x[1] - x[0])
+    return ins[j:i + 1]
 
 
 def klass(op):
