@@ -159,6 +159,41 @@ def test_wide_direct_lut_models(ctx, total):
             assert (dec[k] == d).all(), k
 
 
+@pytest.mark.parametrize("total,c_big", [(65536, 65536 - 255), (32768, 32768 - 255),
+                                         (4096, 4096 - 255), (65536, 1 << 15)])
+@pytest.mark.parametrize("misalign", [False, True])
+def test_rare_heavy_models(ctx, total, c_big, misalign):
+    """Small models whose coded symbols are nearly all c = 1 of a large total: every symbol
+    narrows range by up to 2^16, so 2-3 bytes settle per symbol and range_reduction_expansion
+    runs often, back to back (the encoder's ring margin between flush checks, the decoders' rare
+    paths and ring checks).  Whole 64-symbol tiles and ragged tails, against the oracle."""
+    rng = np.random.default_rng(total + c_big + misalign)
+    c = np.ones(256, np.int64)
+    c[0] = c_big
+    c[1] = total - c_big - 254
+    c = c.astype(np.uint32)
+    cum = cum_of(c)
+    m = rc.StaticModel(c, cum, total)
+    lens = [64, 640, 4096, 4099, 65536, 1000, 127, 0] * 4
+    # symbols 2..255 only (c = 1), with a few runs of the big symbol between them
+    chunks = []
+    for L in lens:
+        ch = rng.integers(2, 256, L)
+        ch[rng.random(L) < 0.05] = 0
+        chunks.append(ch.astype(np.uint8))
+    caps = [rc.slot_capacity(L, m.max_bits_per_symbol() + 1) for L in lens]
+    out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=misalign, seed=total)
+    codes = []
+    for k, ch in enumerate(chunks):
+        f, b, L = cpu.encode(c, cum, total, ch)
+        assert (fl[k], ol[k]) == (f, L), k
+        assert bytes(out[out_off[k]: out_off[k] + ol[k]]) == b, k
+        codes.append(b)
+    dec, fd = run_decode(m, codes, lens, misalign=misalign, seed=total + 1)
+    for k, ch in enumerate(chunks):
+        assert fd[k] == 0 and (dec[k] == ch).all(), k
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_garbage_streams_decode_like_oracle(ctx, seed):
     """find_index on arbitrary bytes (data < lower_bound wraps, rfreq >= total) must pick the
