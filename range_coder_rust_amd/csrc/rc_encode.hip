@@ -192,6 +192,31 @@ static __device__ __forceinline__ void enc_sym(Enc& e, const ModelArgs& m, uint2
   }
 }
 
+// Two symbols with ONE rare test (SM models; ENC_PAIR): the second symbol is coded from the
+// first's state before its range_reduction_expansion, which is exact for every lane that did not
+// need one; a lane that did restores the state after the first symbol (still in registers),
+// expands it and codes the second again.  Its speculative ring store went to a slot the redo
+// rewrites (the redo's bytes start at the same bit position), so nothing else needs undoing.
+// Halves the per-symbol wave-uniform branches, which cost the encoder ~8%.
+template <int DIV, int SM>
+static __device__ __forceinline__ void enc_sym2(Enc& e, const ModelArgs& m, uint2 t0, uint2 t1,
+                                                bool act, u32 lane, const u32* wring,
+                                                const EncOut* wout) {
+  bool r0 = false, r1 = false;
+  if (act) r0 = enc_step<DIV, SM>(e, m, t0);
+  const Enc ea = e;
+  if (act) r1 = enc_step<DIV, SM>(e, m, t1);
+  if (__builtin_expect(__any((int)(r0 | r1)), 0)) {
+    if (r0) {
+      e = ea;
+      enc_rare(e);
+      r1 = enc_step<DIV, SM>(e, m, t1);
+    }
+    if (r1) enc_rare(e);
+    enc_flush(e, lane, wring, wout);
+  }
+}
+
 // 16 symbols from one 16-B load, a flush check after every 8 (wave-uniform).  The table entry
 // of the next symbol is read before the current symbol is coded, so the LDS latency is off the
 // range -> range dependency chain.
@@ -205,12 +230,24 @@ static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const u
   uint2 t = s_tab[w0 & 255u];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
+    if (ENC_PAIR && SM) {
+      // table entries two symbols ahead (the pair's second and the next pair's first)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const u32 sn = i < 3 ? (w0 >> (8 * (i + 1))) & 255u : w1 & 255u;
-      const uint2 tn = s_tab[sn];  // (past the tile's end: a harmless extra read)
-      enc_sym<DIV, SM>(e, m, t, act, lane, wring, wout);
-      t = tn;
+      for (int i = 0; i < 4; i += 2) {
+        const uint2 t1 = s_tab[(w0 >> (8 * (i + 1))) & 255u];
+        const u32 sn = i < 2 ? (w0 >> (8 * (i + 2))) & 255u : w1 & 255u;
+        const uint2 tn = s_tab[sn];  // (past the tile's end: a harmless extra read)
+        enc_sym2<DIV, SM>(e, m, t, t1, act, lane, wring, wout);
+        t = tn;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const u32 sn = i < 3 ? (w0 >> (8 * (i + 1))) & 255u : w1 & 255u;
+        const uint2 tn = s_tab[sn];  // (past the tile's end: a harmless extra read)
+        enc_sym<DIV, SM>(e, m, t, act, lane, wring, wout);
+        t = tn;
+      }
     }
     if (q & 1) enc_flush(e, lane, wring, wout);
     w0 = w1;

@@ -44,6 +44,9 @@
 #ifndef DEC_SPEC
 #define DEC_SPEC 1           // every SM decoder takes the speculative step (verify deferred)
 #endif
+#ifndef ENC_PAIR
+#define ENC_PAIR 1           // small-model encoders test the rare path once per two symbols
+#endif
 #ifndef DEC_TAB_LDS
 #define DEC_TAB_LDS 1        // direct-LUT decoders: keep the (cum, c) table in LDS too
 #endif
