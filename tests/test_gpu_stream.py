@@ -486,3 +486,51 @@ def test_cpp_find_index(ctx):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "find_index called 16 times" in r.stdout and "test passed" in r.stdout
+
+
+def test_threads_share_the_default_context(ctx):
+    """Several Python threads code their own streams through the process-wide default context at
+    the same time (ctypes releases the GIL in every native call): each stream's staging block
+    use is serialised per context (rc_resume.hip), so no thread sees another's bytes.  Static
+    tables decode ahead in blocks and encoders flush at every peek_code, so every thread goes
+    through the staging block many times."""
+    import threading
+
+    n_threads, n_sym = 4, 6000
+    tables, streams = [], []
+    for k in range(n_threads):
+        rng = np.random.default_rng(100 + k)
+        counts = [int(x) for x in rng.integers(1, 50, 40 + 20 * k)]
+        tables.append(rc.FreqTable.from_counts(counts))
+        p = np.asarray(counts, float) / sum(counts)
+        streams.append([int(s) for s in rng.choice(len(counts), n_sym, p=p)])
+    codes, decoded, errors = [None] * n_threads, [None] * n_threads, []
+    start = threading.Barrier(n_threads)
+
+    def work(k):
+        try:
+            t, syms = tables[k], streams[k]
+            start.wait()
+            e = rc.Encoder()
+            for i, s in enumerate(syms):
+                e.encode(t, s)
+                if i % 750 == 749:
+                    e.peek_code()
+            codes[k] = e.finish()
+            d = rc.Decoder(codes[k])
+            decoded[k] = [d.decode(t) for _ in syms]
+        except Exception as exc:  # noqa: BLE001 (reported below)
+            errors.append((k, repr(exc)))
+
+    threads = [threading.Thread(target=work, args=(k,)) for k in range(n_threads)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not errors, errors
+    for k in range(n_threads):
+        c = np.asarray(tables[k].c, np.uint32)
+        cum = np.asarray(tables[k].cum, np.uint32)
+        f, b, _ = cpu.encode(c, cum, tables[k].total, np.asarray(streams[k], np.uint8))
+        assert f == 0 and bytes(codes[k]) == bytes(b), k
+        assert decoded[k] == streams[k], k
