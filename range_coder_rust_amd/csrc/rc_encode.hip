@@ -89,8 +89,13 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
 // flush rounds until no lane's ring is above the threshold (wave-uniform call sites only)
 static __device__ __forceinline__ void enc_flush(Enc& e, u32 lane, const u32* wring,
                                                  const EncOut* wout) {
-  while (__any((int)(enc_wpos(e) - e.fpos >= FLUSH_AT)))
-    enc_round(e, enc_wpos(e) - e.fpos >= ENC_UNIT, lane, wring, wout);
+  // (the first test stays inline in every caller: written as a plain while loop, the compiler
+  // shared one test block among the call sites and copied the coder state at each jump to it)
+  if (__builtin_expect(__any((int)(enc_wpos(e) - e.fpos >= FLUSH_AT)), 0)) {
+    do {
+      enc_round(e, enc_wpos(e) - e.fpos >= ENC_UNIT, lane, wring, wout);
+    } while (__any((int)(enc_wpos(e) - e.fpos >= FLUSH_AT)));
+  }
 }
 
 // One settled byte, with a conditional push (rare paths only).
