@@ -691,8 +691,8 @@ static __device__ __forceinline__ void win_step(ADec& d, const ACode& g, u32 nb)
   const u32 c2 = d.cpos + nb;
   u32 mc, d2n;  // mc = ~0: crossed into the next dword (bit 2 of the position flipped)
   asm("v_bfe_i32 %0, %1, 2, 1" : "=v"(mc) : "v"(d.cpos ^ c2));
-  d.D0 = msel(mc, d.D1, d.D0);
-  d.D1 = msel(mc, d.D2, d.D1);
+  d.D0 = mselc(mc, d.D1, d.D0);
+  d.D1 = mselc(mc, d.D2, d.D1);
   asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(d2n) : "v"(mc), "v"(d.d2o));  // d2o + 4 if crossed
   d.d2o = min(d2n, g.dwl);
   d.D2 = ldw(g, d.d2o);
@@ -719,31 +719,31 @@ static __device__ __forceinline__ void dec_walk(DWalk& w, const ADec& d, u32 q, 
   {                                                     \
     const u32 v_ = (V), nd_ = v_ + nrem;                \
     mr[l] = smask(nd_);                                 \
-    w.nv[l] = v_ + msel(mr[l], 0u, inc);                \
+    w.nv[l] = v_ + mselc(mr[l], 0u, inc);                \
     w.P[l] = P;                                         \
     nrem = max(nrem, nd_);                              \
     e1 = min(e1, nd_);                                  \
     P |= mr[l] & ((128u >> (l)) * 128u);                \
   }
   RC_LEVEL(0, d.L0)
-  RC_LEVEL(1, msel(mr[0], d.L1b, d.L1a))
+  RC_LEVEL(1, mselc(mr[0], d.L1b, d.L1a))
   {
-    const u32 t0 = msel(mr[0], d.L2c, d.L2a), t1 = msel(mr[0], d.L2d, d.L2b);
-    RC_LEVEL(2, msel(mr[1], t1, t0))
+    const u32 t0 = mselc(mr[0], d.L2c, d.L2a), t1 = mselc(mr[0], d.L2d, d.L2b);
+    RC_LEVEL(2, mselc(mr[1], t1, t0))
   }
   {  // levels 3-5: one 7-node read below P
     const u32 r3 = lrd(P + ROW(16)), r4a = lrd(P + ROW(8)), r4b = lrd(P + ROW(24));
     const u32 r5a = lrd(P + ROW(4)), r5b = lrd(P + ROW(12));
     const u32 r5c = lrd(P + ROW(20)), r5d = lrd(P + ROW(28));
     RC_LEVEL(3, r3)
-    RC_LEVEL(4, msel(mr[3], r4b, r4a))
-    const u32 u0 = msel(mr[3], r5c, r5a), u1 = msel(mr[3], r5d, r5b);
-    RC_LEVEL(5, msel(mr[4], u1, u0))
+    RC_LEVEL(4, mselc(mr[3], r4b, r4a))
+    const u32 u0 = mselc(mr[3], r5c, r5a), u1 = mselc(mr[3], r5d, r5b);
+    RC_LEVEL(5, mselc(mr[4], u1, u0))
   }
   {  // levels 6-7: one 3-node read
     const u32 r6 = lrd(P + ROW(2)), r7a = lrd(P + ROW(1)), r7b = lrd(P + ROW(3));
     RC_LEVEL(6, r6)
-    RC_LEVEL(7, msel(mr[6], r7b, r7a))
+    RC_LEVEL(7, mselc(mr[6], r7b, r7a))
   }
 #undef RC_LEVEL
   w.s = (P - col) >> 7;

@@ -79,6 +79,12 @@ static __device__ __forceinline__ u32 msel(u32 m, u32 a, u32 b) {
   return r;
 }
 
+// msel from C: with the mask opaque (smask, or masks the compiler cannot trace to a compare) it
+// compiles to one v_bfi_b32 / v_bitop3_b32, and unlike the asm form its consumers are not padded
+// (the hazard recognizer cannot see into inline asm, so it puts an s_nop before the next
+// dependent VOP1/VOP2 instruction)
+static __device__ __forceinline__ u32 mselc(u32 m, u32 a, u32 b) { return (a & m) | (b & ~m); }
+
 // the sign of v as a mask (0 / ~0), opaque to the compiler (which otherwise turns selects on it
 // back into v_cmp + v_cndmask_b32 on VCC)
 static __device__ __forceinline__ u32 smask(u32 v) {

@@ -163,7 +163,8 @@ static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint
   // no_carry_expansion in closed form: k = clz(low ^ upper) / 8 bytes settle (<= 3 here;
   // equal high halves (ffbh = ~0) mean >= 4 and the rare path continues after these 3)
   const u32 lh = hi32(e.low);
-  const u32 z = ffbh(lh ^ hi32(e.low + e.range));
+  // (SM: the high halves differ, so clz of a nonzero value, as a builtin: asm would be padded)
+  const u32 z = SM ? (u32)__builtin_clz(lh ^ hi32(e.low + e.range)) : ffbh(lh ^ hi32(e.low + e.range));
   const u32 nb = z & 24u;
   const u32 bytes = __builtin_amdgcn_ubfe(lh, 32u - nb, nb);  // the top nb bits (0 if nb == 0)
   e.acc = (e.acc << nb) | bytes;

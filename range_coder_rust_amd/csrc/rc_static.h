@@ -99,6 +99,9 @@ static __device__ __forceinline__ u64 range_par_total(u64 range, const ModelArgs
   return rem >= (u64)m.total ? q + 1 : q;
 }
 
+#ifndef MAD24_C
+#define MAD24_C 1  // the 24-bit high-half mad from C (inline asm makes the hazard recognizer pad)
+#endif
 // r * v for the coder's products (range_coder.rs:65, :70).  SM (256 <= total <= 2^16): r < 2^56
 // and v <= 2^16, so the high half is a 24-bit multiply.  SM is written out as two
 // instructions, lo(r)*v as a 64-bit product plus a 24-bit mad into its high half: from the C
@@ -110,7 +113,8 @@ static __device__ __forceinline__ u64 mul_rv(u64 r, u32 v) {
     u64 p, c;
     u32 h;
     asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(c) : "v"((u32)r), "v"(v));
-    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(r)), "v"(v), "v"(hi32(p)));
+    h = MAD24_C ? __umul24(hi32(r), v) + hi32(p) : 0u;
+    if (!MAD24_C) asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(r)), "v"(v), "v"(hi32(p)));
     return ((u64)h << 32) | (u32)p;
   }
   return r * (u64)v;
@@ -124,7 +128,8 @@ static __device__ __forceinline__ u64 mad_rv(u64 r, u32 v, u64 a) {
     u64 p, c;
     u32 h;
     asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(p), "=s"(c) : "v"((u32)r), "v"(v), "v"(a));
-    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(r)), "v"(v), "v"(hi32(p)));
+    h = MAD24_C ? __umul24(hi32(r), v) + hi32(p) : 0u;
+    if (!MAD24_C) asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(r)), "v"(v), "v"(hi32(p)));
     return ((u64)h << 32) | (u32)p;
   }
   return r * (u64)v + a;
