@@ -645,7 +645,7 @@ static __device__ __forceinline__ u64 mul_rs(u64 r, u32 v) {
     u64 p, c;
     u32 h;
     asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(c) : "v"((u32)r), "v"(v));
-    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(r)), "v"(v), "v"(hi32(p)));
+    h = __umul24(hi32(r), v) + hi32(p);  // (C, not asm: see MAD24_C in rc_static.h)
     return ((u64)h << 32) | (u32)p;
   }
   return mul_r(r, v);
