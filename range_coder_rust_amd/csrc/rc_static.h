@@ -47,6 +47,9 @@
 #ifndef ENC_PAIR
 #define ENC_PAIR 1           // small-model encoders test the rare path once per two symbols
 #endif
+#ifndef DEC_CHECK_SPAN
+#define DEC_CHECK_SPAN 8     // small-model decoders: symbols between ring checks in a phase
+#endif
 #ifndef DEC_TAB_LDS
 #define DEC_TAB_LDS 1        // direct-LUT decoders: keep the (cum, c) table in LDS too
 #endif
