@@ -1,4 +1,7 @@
-# scratch: cost of the per-symbol rare branch at the N = 8 shard (2^17) and at 2^20 (Zipf)
+# scratch: cost of the per-symbol rare branch at the N = 8 shard (2^17) and at 2^20 (Zipf).
+# The variants it compared were built with -DRC_EXP_NOBRANCH=1 / -DRC_EXP_RAREBODY=1,2, scratch
+# switches removed from the sources after the measurement (DESIGN.md §5,
+# profiles/r03/ab/branch_cost/); kept as the record of how the numbers were taken.
 O=$GRAFT_REPO_ROOT/gpurun_out/exp_nb
 mkdir -p $O
 ONE="--no-cpu-baseline --no-adaptive --no-model-build --no-container --no-host-stream"
