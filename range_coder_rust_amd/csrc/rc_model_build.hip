@@ -5,7 +5,7 @@
 // add_alphabet_freq per symbol (examples/sample_impl.rs:49-60), then calc_cum's exclusive scan
 // (:61-69).  Here:
 //   * k_histogram counts symbols of many chunks at once (per-chunk and/or batch histograms):
-//     pure HBM streaming, 16-B loads, LDS sub-histograms;
+//     16-B loads, eight u16 LDS sub-histograms per wave;
 //   * rc_quantize_counts turns counts into a (c, cum, total) table: exactly calc_cum's table
 //     when no target is given, or a table scaled to a target total (e.g. 2^16, so the coder
 //     takes its fast power-of-two path), deterministic and restated by the oracle;
@@ -19,53 +19,101 @@
 #include <algorithm>
 #include <vector>
 
-#define HWG 256
-#define HCOPIES 4  // sub-histograms per wave, interleaved per bin: lanes L, L+1, L+2, L+3 that
-                   // hit one symbol land in 4 different banks
+#define HWG 256  // k_ideal_bits
 
-// chunk-stride grid: each WG counts whole chunks into LDS, flushes each chunk's 256 counts
-// (chunk_hist, optional) and accumulates its bins in registers for one final global atomic
-// per bin (hist, optional)
-__global__ __launch_bounds__(HWG) void k_histogram(const uint8_t* __restrict__ syms,
+// k_histogram: chunk-stride workgroups of 4 waves; 16-B loads; LDS sub-histograms counted with
+// ds_add_u32.  Measured (profiles/r03/ab/hist/): the LDS atomics' latency per
+// wave binds, so the rate follows the resident waves per CU, and lanes of one instruction that
+// hit one address serialise (a skewed model's hot symbols).  Hence small sub-histograms (4 KiB
+// per wave: 32 waves per CU) with many copies: u16 counters, eight copies.
+typedef __attribute__((address_space(3))) u32 hl_u32;
+
+static __device__ __forceinline__ void hl_add(hl_u32* p, u32 v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// Eight u16 sub-histograms per wave in the LDS of four u32 ones (4 KiB per wave, so 32 waves
+// per CU as with four): lane L counts into copy L & 7; dword 8 (b & 127) + copy holds bins b
+// (low half) and b + 128 (high half), so the hot low symbols of a skewed model never share a
+// dword.  A u16 takes at most 8 lanes x HSEG_LANE symbols before the segment's readout.
+#define HSEG_LANE 8176u  // symbols per lane per segment (16 x 511): 8 x (8176 + 2) < 2^16
+__global__ __launch_bounds__(256) void k_histogram(const uint8_t* __restrict__ syms,
                                                    const u64* __restrict__ sym_off,
                                                    u32 n_chunks, u32* __restrict__ chunk_hist,
                                                    u64* __restrict__ hist) {
-  __shared__ u32 sh[(HWG / 64) * 256 * HCOPIES];
+  __shared__ u32 sh[4 * 1024];
   const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  u32* my = sh + wave * 256 * HCOPIES + (lane & (HCOPIES - 1));
+  // LDS byte address of this lane's copy; a VGPR holding 1 (the SDWA shift's operand)
+  const u32 colb = (u32)(uintptr_t)(hl_u32*)(sh + wave * 1024 + (lane & 7));
+  u32 one = 1;
+  asm volatile("" : "+v"(one));
   RC_VGPR_FLOOR_64();
   u64 acc = 0;  // bin tid over this WG's chunks
+  for (u32 j = tid; j < 4 * 1024; j += 256) sh[j] = 0;
   for (u32 k = blockIdx.x; k < n_chunks; k += gridDim.x) {
-    for (u32 j = tid; j < (HWG / 64) * 256 * HCOPIES; j += HWG) sh[j] = 0;
-    __syncthreads();
     const u64 s0 = sym_off[k], n = sym_off[k + 1] - s0;
     const uint8_t* p = syms + s0;
     u64 head = (16 - ((uintptr_t)p & 15)) & 15;
     if (head > n) head = n;
-    if (tid < head) atomicAdd(&my[(u32)p[tid] * HCOPIES], 1u);
     const u64 nv = (n - head) >> 4;
     const u32x4* v = reinterpret_cast<const u32x4*>(p + head);
-#pragma unroll 4
-    for (u64 i = tid; i < nv; i += HWG) {
-      const u32x4 w = gload16(v + i);
-      const u32 ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) atomicAdd(&my[((ws[q] >> (8 * b)) & 255u) * HCOPIES], 1u);
-      }
-    }
-    for (u64 i = head + (nv << 4) + tid; i < n; i += HWG) atomicAdd(&my[(u32)p[i] * HCOPIES], 1u);
-    __syncthreads();
     u32 cnt = 0;
+    // segments of 256 * HSEG_LANE / 16 blocks: every lane adds <= HSEG_LANE symbols per segment
+    const u64 seg = 256ull * HSEG_LANE / 16;
+    for (u64 b0 = 0; b0 == 0 || b0 < nv; b0 += seg) {
+      __syncthreads();
+      if (b0 == 0) {
+        if (tid < head) {
+          const u32 b = p[tid];
+          atomicAdd(&sh[wave * 1024 + (b & 127) * 8 + (lane & 7)], 1u << (16 * (b >> 7)));
+        }
+        const u64 t0 = head + (nv << 4);
+        if (t0 + tid < n) {  // < 16 tail symbols
+          const u32 b = p[t0 + tid];
+          atomicAdd(&sh[wave * 1024 + (b & 127) * 8 + (lane & 7)], 1u << (16 * (b >> 7)));
+        }
+      }
+      const u64 b1 = b0 + seg < nv ? b0 + seg : nv;
+#pragma unroll 4
+      for (u64 i = b0 + tid; i < b1; i += 256) {
+        const u32x4 w = gload16(v + i);
+        const u32 ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-    for (u32 w = 0; w < HWG / 64; ++w) {
+        for (int q = 0; q < 4; ++q) {
+          // per symbol: the dword's address as one bfe + one v_lshl_add_u32, the increment as
+          // one SDWA shift reading byte j of x = 16 (b_j >> 7) per byte (asm: from C the
+          // compiler re-derived each shift from the word with a shift, an and and an add)
+          const u32 x = (ws[q] >> 3) & 0x10101010u;
+          u32 a[4], y[4];
+#define H8_SYM(j)                                                                               \
+  asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(a[j]) : "v"(__builtin_amdgcn_ubfe(ws[q], 8 * j, 7)), \
+      "v"(colb));                                                                               \
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #j    \
+      " src1_sel:DWORD"                                                                         \
+      : "=v"(y[j]) : "v"(x), "v"(one));                                                        \
+  hl_add((hl_u32*)(uintptr_t)a[j], y[j]);
+          H8_SYM(0) H8_SYM(1) H8_SYM(2) H8_SYM(3)
+#undef H8_SYM
+        }
+      }
+      __syncthreads();
+      // bin tid: the half (tid >> 7) of dwords 8 (tid & 127) + c of the four waves
 #pragma unroll
-      for (u32 c = 0; c < HCOPIES; ++c) cnt += sh[w * 256 * HCOPIES + tid * HCOPIES + c];
+      for (u32 w = 0; w < 4; ++w) {
+        u32x4* r = reinterpret_cast<u32x4*>(sh + w * 1024 + (tid & 127) * 8);
+#pragma unroll
+        for (u32 h = 0; h < 2; ++h) {
+          const u32x4 x = r[h];
+          const u32 sft = 16 * (tid >> 7);
+          cnt += ((x.x >> sft) & 0xFFFFu) + ((x.y >> sft) & 0xFFFFu) + ((x.z >> sft) & 0xFFFFu) +
+                 ((x.w >> sft) & 0xFFFFu);
+        }
+      }
+      __syncthreads();
+      for (u32 j = tid; j < 4 * 1024; j += 256) sh[j] = 0;
     }
     if (chunk_hist) chunk_hist[(u64)k * 256 + tid] = cnt;
     acc += cnt;
-    __syncthreads();
   }
   if (hist && acc) atomicAdd(reinterpret_cast<unsigned long long*>(hist + tid), (unsigned long long)acc);
 }
@@ -134,8 +182,9 @@ rc_status rc_histogram(rc_ctx* ctx, const uint8_t* syms, const uint64_t* sym_off
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return RC_E_DEVICE;
-  const u32 grid = std::min<u32>(n_chunks, (u32)cus * 8);  // 16 KiB LDS/WG: 8 WGs per CU
-  hipLaunchKernelGGL(k_histogram, dim3(grid), dim3(HWG), 0, s, syms, sym_off, n_chunks,
+  // 16 KiB LDS per workgroup: 8 workgroups (32 waves) per CU
+  const u32 grid = std::min<u32>(n_chunks, (u32)cus * 8);
+  hipLaunchKernelGGL(k_histogram, dim3(grid), dim3(256), 0, s, syms, sym_off, n_chunks,
                      chunk_hist, hist);
   return hipGetLastError() == hipSuccess ? RC_OK : RC_E_DEVICE;
 }

@@ -70,6 +70,57 @@ def test_histogram_large_chunks_and_accumulation(ctx):
     assert torch.equal(h2, 2 * hist)
 
 
+def _data(rng, kind, tot):
+    if kind == "uniform":
+        return rng.integers(0, 256, tot).astype(np.uint8)
+    if kind == "zipf":
+        c, _, _ = synth.zipf_table()
+        return rng.choice(256, tot, p=np.asarray(c, float) / np.sum(c)).astype(np.uint8)
+    if kind == "constant":  # every symbol of every lane into one u16 counter
+        return np.full(tot, 0xA7, np.uint8)
+    # bins b and b + 128 share a counter dword (low and high halves)
+    return np.where(rng.random(tot) < 0.5, 0x05, 0x85).astype(np.uint8)
+
+
+def _check_hist(data, off):
+    hist, ch = rc.histogram(dev(data), dev(off), per_chunk=True)
+    torch.cuda.synchronize()
+    ch = ch.cpu().numpy()
+    for k in range(len(off) - 1):
+        want = np.bincount(data[off[k]:off[k + 1]], minlength=256)
+        assert (ch[k] == want).all(), k
+    want_all = np.bincount(data[off[0]:off[-1]], minlength=256)
+    assert (hist.cpu().numpy() == want_all).all()
+    hist_only, _ = rc.histogram(dev(data), dev(off), per_chunk=False)
+    assert (hist_only.cpu().numpy() == want_all).all()
+
+
+@pytest.mark.parametrize("base", [0, 7])
+@pytest.mark.parametrize("kind", ["uniform", "zipf", "constant", "pair"])
+def test_histogram_skewed_and_paired_bins(ctx, base, kind):
+    """k_histogram's u16 sub-histograms: ragged chunks with unaligned starts, data that puts
+    every symbol into one counter, and two bins sharing one counter dword."""
+    rng = np.random.default_rng(base + 100 * len(kind))
+    lens = rng.integers(0, 70000, 90)
+    lens[::9] = 0
+    tot = int(lens.sum()) + base
+    data = _data(rng, kind, tot)
+    _check_hist(data, np.concatenate([[0], np.cumsum(lens)]).astype(np.int64) + base)
+
+
+@pytest.mark.parametrize("kind", ["constant", "pair", "zipf"])
+def test_histogram_multi_segment_chunks(ctx, kind):
+    """Chunks longer than one counting segment (256 x 8176 symbols, ~2 MiB): the u16 counters
+    are read out and cleared between segments, so even a one-symbol chunk of 5 MiB is exact."""
+    rng = np.random.default_rng(len(kind))
+    seg = 256 * 8176
+    lens = np.array([seg - 1, seg, seg + 1, 2 * seg + 17, 5 << 20, 3, 0, seg + 15], np.int64)
+    base = 5
+    tot = int(lens.sum()) + base
+    data = _data(rng, kind, tot)
+    _check_hist(data, np.concatenate([[0], np.cumsum(lens)]).astype(np.int64) + base)
+
+
 @pytest.mark.parametrize("T,all_symbols", [(0, False), (1 << 16, True), (4096, False),
                                            (1 << 20, True)])
 def test_build_model_table_and_round_trip(ctx, T, all_symbols):
