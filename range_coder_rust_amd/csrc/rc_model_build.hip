@@ -14,6 +14,7 @@
 #include "rc_common.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -37,11 +38,49 @@ static __device__ __forceinline__ void hl_add(hl_u32* p, u32 v) {
 // (low half) and b + 128 (high half), so the hot low symbols of a skewed model never share a
 // dword.  A u16 takes at most 8 lanes x HSEG_LANE symbols before the segment's readout.
 #define HSEG_LANE 8176u  // symbols per lane per segment (16 x 511): 8 x (8176 + 2) < 2^16
-__global__ __launch_bounds__(256) void k_histogram(const uint8_t* __restrict__ syms,
-                                                   const u64* __restrict__ sym_off,
-                                                   u32 n_chunks, u32* __restrict__ chunk_hist,
-                                                   u64* __restrict__ hist) {
+
+// blocks [i0, i1) of the chunk (stride 256 from this thread's first) into the sub-histograms.
+// HOT: symbol H (wave-uniform) is not added to LDS but counted by ballot into hc (an SGPR):
+// the lanes of a skewed model's hottest symbol no longer serialise on its counters.
+template <bool HOT>
+static __device__ __forceinline__ void h8_blocks(const u32x4* v, u64 i0, u64 i1, u32 colb, u32 one,
+                                                 u32 H, u32& hc) {
+#pragma unroll 4
+  for (u64 i = i0; i < i1; i += 256) {
+    const u32x4 w = gload16(v + i);
+    const u32 ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // per symbol: the dword's address as one bfe + one v_lshl_add_u32, the increment as
+      // one SDWA shift reading byte j of x = 16 (b_j >> 7) per byte (asm: from C the
+      // compiler re-derived each shift from the word with a shift, an and and an add)
+      const u32 x = (ws[q] >> 3) & 0x10101010u;
+      u32 a[4], y[4];
+#define H8_SYM(j)                                                                               \
+  asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(a[j]) : "v"(__builtin_amdgcn_ubfe(ws[q], 8 * j, 7)), \
+      "v"(colb));                                                                               \
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #j    \
+      " src1_sel:DWORD"                                                                         \
+      : "=v"(y[j]) : "v"(x), "v"(one));                                                        \
+  if (HOT) {                                                                                    \
+    const bool h = __builtin_amdgcn_ubfe(ws[q], 8 * j, 8) == H;                                 \
+    hc += (u32)__builtin_popcountll(__builtin_amdgcn_ballot_w64(h));                            \
+    if (!h) hl_add((hl_u32*)(uintptr_t)a[j], y[j]);                                             \
+  } else {                                                                                      \
+    hl_add((hl_u32*)(uintptr_t)a[j], y[j]);                                                     \
+  }
+      H8_SYM(0) H8_SYM(1) H8_SYM(2) H8_SYM(3)
+#undef H8_SYM
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_histogram(
+    const uint8_t* __restrict__ syms, const u64* __restrict__ sym_off, u32 n_chunks,
+    u32* __restrict__ chunk_hist, u64* __restrict__ hist, u32 hot_ok) {
   __shared__ u32 sh[4 * 1024];
+  __shared__ u32 s_hot[4];  // per wave: the segment's ballot count of the hot symbol
+  __shared__ u32 s_key[4];  // per wave: max of (count << 8 | bin) of the last chunk
   const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // LDS byte address of this lane's copy; a VGPR holding 1 (the SDWA shift's operand)
   const u32 colb = (u32)(uintptr_t)(hl_u32*)(sh + wave * 1024 + (lane & 7));
@@ -50,6 +89,7 @@ __global__ __launch_bounds__(256) void k_histogram(const uint8_t* __restrict__ s
   RC_VGPR_FLOOR_64();
   u64 acc = 0;  // bin tid over this WG's chunks
   for (u32 j = tid; j < 4 * 1024; j += 256) sh[j] = 0;
+  bool have_key = false;
   for (u32 k = blockIdx.x; k < n_chunks; k += gridDim.x) {
     const u64 s0 = sym_off[k], n = sym_off[k + 1] - s0;
     const uint8_t* p = syms + s0;
@@ -60,9 +100,16 @@ __global__ __launch_bounds__(256) void k_histogram(const uint8_t* __restrict__ s
     u32 cnt = 0;
     // segments of 256 * HSEG_LANE / 16 blocks: every lane adds <= HSEG_LANE symbols per segment
     const u64 seg = 256ull * HSEG_LANE / 16;
+    u32 H = 256, key = 0;
     for (u64 b0 = 0; b0 == 0 || b0 < nv; b0 += seg) {
       __syncthreads();
       if (b0 == 0) {
+        // the hot symbol: the previous chunk's most frequent one, if it held >= 1/8 of it
+        if (have_key && hot_ok) {
+          key = max(max(s_key[0], s_key[1]), max(s_key[2], s_key[3]));
+          key = __builtin_amdgcn_readfirstlane(key);
+        }
+        H = key >> 8 ? (key & 255u) : 256u;
         if (tid < head) {
           const u32 b = p[tid];
           atomicAdd(&sh[wave * 1024 + (b & 127) * 8 + (lane & 7)], 1u << (16 * (b >> 7)));
@@ -74,28 +121,10 @@ __global__ __launch_bounds__(256) void k_histogram(const uint8_t* __restrict__ s
         }
       }
       const u64 b1 = b0 + seg < nv ? b0 + seg : nv;
-#pragma unroll 4
-      for (u64 i = b0 + tid; i < b1; i += 256) {
-        const u32x4 w = gload16(v + i);
-        const u32 ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          // per symbol: the dword's address as one bfe + one v_lshl_add_u32, the increment as
-          // one SDWA shift reading byte j of x = 16 (b_j >> 7) per byte (asm: from C the
-          // compiler re-derived each shift from the word with a shift, an and and an add)
-          const u32 x = (ws[q] >> 3) & 0x10101010u;
-          u32 a[4], y[4];
-#define H8_SYM(j)                                                                               \
-  asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(a[j]) : "v"(__builtin_amdgcn_ubfe(ws[q], 8 * j, 7)), \
-      "v"(colb));                                                                               \
-  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #j    \
-      " src1_sel:DWORD"                                                                         \
-      : "=v"(y[j]) : "v"(x), "v"(one));                                                        \
-  hl_add((hl_u32*)(uintptr_t)a[j], y[j]);
-          H8_SYM(0) H8_SYM(1) H8_SYM(2) H8_SYM(3)
-#undef H8_SYM
-        }
-      }
+      u32 hc = 0;
+      if (H < 256) h8_blocks<true>(v, b0 + tid, b1, colb, one, H, hc);
+      else h8_blocks<false>(v, b0 + tid, b1, colb, one, H, hc);
+      if (lane == 0) s_hot[wave] = hc;
       __syncthreads();
       // bin tid: the half (tid >> 7) of dwords 8 (tid & 127) + c of the four waves
 #pragma unroll
@@ -109,11 +138,19 @@ __global__ __launch_bounds__(256) void k_histogram(const uint8_t* __restrict__ s
                  ((x.w >> sft) & 0xFFFFu);
         }
       }
+      if (tid == H) cnt += s_hot[0] + s_hot[1] + s_hot[2] + s_hot[3];
       __syncthreads();
       for (u32 j = tid; j < 4 * 1024; j += 256) sh[j] = 0;
     }
     if (chunk_hist) chunk_hist[(u64)k * 256 + tid] = cnt;
     acc += cnt;
+    // this chunk's most frequent symbol, for the next one (read after the next barrier); a
+    // bin below 1/8 of the chunk gives key 0 (no hot symbol)
+    u32 kv = (u64)cnt * 8 >= n && n >= 4096 ? (min(cnt, 0xFFFFFFu) << 8) | tid : 0u;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) kv = max(kv, (u32)__shfl_xor((int)kv, o));
+    if (lane == 0) s_key[wave] = kv;
+    have_key = true;
   }
   if (hist && acc) atomicAdd(reinterpret_cast<unsigned long long*>(hist + tid), (unsigned long long)acc);
 }
@@ -184,8 +221,10 @@ rc_status rc_histogram(rc_ctx* ctx, const uint8_t* syms, const uint64_t* sym_off
     return RC_E_DEVICE;
   // 16 KiB LDS per workgroup: 8 workgroups (32 waves) per CU
   const u32 grid = std::min<u32>(n_chunks, (u32)cus * 8);
+  // RC_HIST_HOT=0 turns the ballot-counted hot symbol off (measurements)
+  const char* hot = getenv("RC_HIST_HOT");
   hipLaunchKernelGGL(k_histogram, dim3(grid), dim3(256), 0, s, syms, sym_off, n_chunks,
-                     chunk_hist, hist);
+                     chunk_hist, hist, (u32)!(hot && *hot == '0'));
   return hipGetLastError() == hipSuccess ? RC_OK : RC_E_DEVICE;
 }
 

@@ -1,4 +1,5 @@
-"""A/B of the histogram kernels (RC_HIST_MODE, in the build that had them: wg4 | h8 | wg8 | pd2) on one box: per-chunk rows and
+"""A/B of the histogram kernels (RC_HIST_MODE, in the build that had them: wg4 | h8 | wg8 | pd2;
+now RC_HIST_HOT: modes nohot | hot) on one box: per-chunk rows and
 the batch histogram of 2^18 x 64 KiB chunks, uniform and Zipf(1.2); exactness vs torch.bincount."""
 import json
 import os
@@ -22,8 +23,9 @@ for data in ("uniform", "zipf"):
     else:
         synth.fill(ctx, 11, synth.inverse_cdf([1] * 256), syms, L, n)
     want = torch.bincount(syms, minlength=256).to(torch.int64)
-    for mode in sys.argv[1:] or ["wg4", "h8", "wg8", "pd2"]:
+    for mode in sys.argv[1:] or ["nohot", "hot"]:
         os.environ["RC_HIST_MODE"] = mode
+        os.environ["RC_HIST_HOT"] = "0" if mode == "nohot" else "1"
         hist, ch = rc.histogram(syms, off, per_chunk=True)
         ok = torch.equal(hist, want) and torch.equal(ch.sum(0, dtype=torch.int64), want)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
