@@ -12,3 +12,6 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 tail -1 $O/smoke.log
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_prof.json 2> $O/bench_prof.err || { tail -20 $O/bench_prof.err; exit 1; }
+find $O/prof -name "*kernel_stats.csv" | head -3
