@@ -141,9 +141,13 @@ __global__ __launch_bounds__(SWG) void k_pack_payload(const uint8_t* __restrict_
                                                       u32 n_chunks, uint8_t* __restrict__ dst,
                                                       const u64* __restrict__ doff,
                                                       u64* __restrict__ index) {
-  const u32 tid = threadIdx.x;
+  // one wave per chunk (four chunks per workgroup in flight, no barriers): a chunk's last
+  // partial round of 16-B granules idles fewer lanes, and one chunk's offset loads overlap the
+  // other waves' copies
+  const u32 tid = threadIdx.x & 63;
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   RC_VGPR_FLOOR_32();
-  for (u32 k = blockIdx.x; k < n_chunks; k += gridDim.x) {
+  for (u32 k = blockIdx.x * (SWG / 64) + wave; k < n_chunks; k += gridDim.x * (SWG / 64)) {
     const u64 l = len[k];
     const uint8_t* sp = slots + slot_off[k];
     uint8_t* dp = dst + doff[k];  // 16-B aligned
@@ -154,8 +158,17 @@ __global__ __launch_bounds__(SWG) void k_pack_payload(const uint8_t* __restrict_
     const u64 ng = pad16(l) >> 4;
     if (((uintptr_t)sp & 15) == 0) {
       const u64 full = l >> 4;  // whole granules inside the stream
-      for (u64 g = tid; g < full; g += SWG)
-        gstore128(dp + 16 * g, gload16(reinterpret_cast<const u32x4*>(sp) + g));
+      const u32x4* src = reinterpret_cast<const u32x4*>(sp);
+      u64 g = tid;
+      for (; g + 192 < full; g += 256) {  // four granules per lane in flight
+        const u32x4 a = gload16(src + g), b = gload16(src + g + 64), c = gload16(src + g + 128),
+                    d = gload16(src + g + 192);
+        gstore128(dp + 16 * g, a);
+        gstore128(dp + 16 * (g + 64), b);
+        gstore128(dp + 16 * (g + 128), c);
+        gstore128(dp + 16 * (g + 192), d);
+      }
+      for (; g < full; g += 64) gstore128(dp + 16 * g, gload16(src + g));
       if (tid == 0 && full < ng) {  // last partial granule: stream bytes, then zeros
         u32 w[4] = {0, 0, 0, 0};
         for (u32 j = 0; j < (u32)(l & 15); ++j) w[j >> 2] |= (u32)sp[16 * full + j] << (8 * (j & 3));
@@ -167,7 +180,7 @@ __global__ __launch_bounds__(SWG) void k_pack_payload(const uint8_t* __restrict_
         gstore128(dp + 16 * full, v);
       }
     } else {  // misaligned slot: dword-assembled granules
-      for (u64 g = tid; g < ng; g += SWG) {
+      for (u64 g = tid; g < ng; g += 64) {
         u32 w[4] = {0, 0, 0, 0};
         for (u32 j = 0; j < 16; ++j) {
           const u64 p = 16 * g + j;
@@ -340,7 +353,7 @@ rc_status rc_container_pack(rc_ctx* ctx, const rc_model* m, const uint8_t* slots
   if (n_chunks) {
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const u32 grid = std::min<u32>(n_chunks, (u32)std::max(cus, 1) * 16);
+    const u32 grid = std::min<u32>((n_chunks + SWG / 64 - 1) / (SWG / 64), (u32)std::max(cus, 1) * 16);
     hipLaunchKernelGGL(k_pack_payload, dim3(grid), dim3(SWG), 0, s, slots_dev, slot_off_dev,
                        code_len_dev, sym_off_dev, n_chunks, dst_dev, doff,
                        reinterpret_cast<u64*>(dst_dev + index_off));
