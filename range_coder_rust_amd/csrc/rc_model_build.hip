@@ -155,33 +155,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   if (hist && acc) atomicAdd(reinterpret_cast<unsigned long long*>(hist + tid), (unsigned long long)acc);
 }
 
-// per chunk: bits = sum_i hist[i] * icl[i] in f64, bins in order 0..255 (icl[i] = +inf for
-// c_i == 0: the reference's ideal_code_length returns Err there, pmodel.rs:16-18).  One thread
-// per chunk; the histogram rows are read through LDS in 256-chunk tiles (coalesced).
+// per chunk: bits = sum_i hist[i] * icl[i] in f64 (icl[i] = +inf for c_i == 0: the reference's
+// ideal_code_length returns Err there, pmodel.rs:16-18).  One wave per chunk: lane L reads bins
+// 4L .. 4L+3 of the row as one 16-B load (the wave reads the whole 1-KiB row at once) and holds
+// their icl in registers for every chunk; the 64 partial sums are added by a butterfly.  Empty
+// bins are skipped (0 * inf would be NaN).
 __global__ __launch_bounds__(HWG) void k_ideal_bits(const double* __restrict__ icl,
                                                     const u32* __restrict__ chunk_hist,
                                                     u32 n_chunks, double* __restrict__ bits) {
-  __shared__ double s_icl[256];
-  __shared__ u32 s_h[HWG][33];  // 32 bins at a time, padded row
-  const u32 tid = threadIdx.x;
-  RC_VGPR_FLOOR_32();
-  s_icl[tid] = icl[tid];
-  const u32 k0 = blockIdx.x * HWG;
-  double acc = 0.0;
-  for (u32 b0 = 0; b0 < 256; b0 += 32) {
-    __syncthreads();
-    // tile: chunk k0 + r, bins b0 .. b0+31; thread t loads (r, c) = (j / 32, j % 32)
-    for (u32 j = tid; j < HWG * 32; j += HWG) {
-      const u32 r = j >> 5, c = j & 31;
-      s_h[r][c] = (k0 + r < n_chunks) ? chunk_hist[(u64)(k0 + r) * 256 + b0 + c] : 0u;
+  const u32 lane = threadIdx.x & 63;
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  RC_VGPR_FLOOR_48();
+  const double i0 = icl[4 * lane], i1 = icl[4 * lane + 1], i2 = icl[4 * lane + 2],
+               i3 = icl[4 * lane + 3];
+  const u32 nw = gridDim.x * (HWG / 64);
+  for (u32 k = blockIdx.x * (HWG / 64) + wave; k < n_chunks; k += nw) {
+    const u32x4 h = gload16(reinterpret_cast<const u32x4*>(chunk_hist + (u64)k * 256) + lane);
+    double acc = 0.0;
+    if (h.x) acc = fma((double)h.x, i0, acc);
+    if (h.y) acc = fma((double)h.y, i1, acc);
+    if (h.z) acc = fma((double)h.z, i2, acc);
+    if (h.w) acc = fma((double)h.w, i3, acc);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+      const u64 v = (u64)__double_as_longlong(acc);
+      const u64 y = ((u64)(u32)__shfl_xor((int)hi32(v), o) << 32) | (u32)__shfl_xor((int)(u32)v, o);
+      acc += __longlong_as_double((long long)y);
     }
-    __syncthreads();
-    for (u32 c = 0; c < 32; ++c) {
-      const u32 h = s_h[tid][c];
-      if (h) acc = fma((double)h, s_icl[b0 + c], acc);
-    }
+    if (lane == 0) bits[k] = acc;
   }
-  if (k0 + tid < n_chunks) bits[k0 + tid] = acc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -323,8 +325,12 @@ rc_status rc_ideal_bits(rc_ctx* ctx, const uint32_t* c_host, uint32_t n_symbols,
     (void)hipFreeAsync(d, s);
     return RC_E_DEVICE;
   }
-  hipLaunchKernelGGL(k_ideal_bits, dim3((n_chunks + HWG - 1) / HWG), dim3(HWG), 0, s, d,
-                     chunk_hist, n_chunks, bits);
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  // one wave per chunk, waves striding over the chunks: 8 workgroups (32 waves) per CU
+  const u32 grid = std::min<u32>((n_chunks + HWG / 64 - 1) / (HWG / 64), (u32)cus * 8);
+  hipLaunchKernelGGL(k_ideal_bits, dim3(grid), dim3(HWG), 0, s, d, chunk_hist, n_chunks, bits);
   const bool ok = hipGetLastError() == hipSuccess;
   // the pinned staging is reused by this thread's next call: wait for the copy
   const bool fr = hipFreeAsync(d, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;

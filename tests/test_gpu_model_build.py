@@ -1,7 +1,8 @@
 """GPU parity of model construction: rc_histogram against numpy
 counts (exact integers), build_model's table against the oracle quantizer, rc_ideal_bits
-against oracle/model_build.ideal_bits (f64; relative tolerance 1e-12, the GPU accumulates with
-fma in bin order, the oracle with separate multiply and add)."""
+against oracle/model_build.ideal_bits (f64; relative tolerance 1e-12: the GPU accumulates four
+bins per lane with fma and adds the 64 lanes by a butterfly, the oracle adds in bin order with
+separate multiply and add; 256 positive terms stay within ~3e-14 either way)."""
 import math
 
 import numpy as np
