@@ -133,7 +133,8 @@ static hipError_t device_scan(hipStream_t s, const u64* v, u32 n, int src, u32 s
 }
 
 // payload gather: chunk k's code (len[k] bytes of its encoder slot) -> dst + doff[k], zero
-// padded to 16 B; index entry k = {symbol count, code length}.  One WG per chunk, grid-stride.
+// padded to 16 B; index entry k = {symbol count, code length}.  One wave per chunk (SWG / 64
+// chunks per workgroup), grid-stride over the chunks.
 __global__ __launch_bounds__(SWG) void k_pack_payload(const uint8_t* __restrict__ slots,
                                                       const u64* __restrict__ slot_off,
                                                       const u64* __restrict__ len,

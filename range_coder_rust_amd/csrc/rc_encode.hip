@@ -14,7 +14,19 @@
 // the per-lane pattern (one 16-B granule of 64 different lines per instruction) cannot.
 // ------------------------------------------------------------------------------------------
 #define ENC_UNIT 64    // bytes per flush unit
-#define FLUSH_AT 88    // ring fill forcing a flush round: 88 + 7*3 + 3 + 11 (rare tail) < 124
+#define FLUSH_AT 88    // ring fill (whole dwords past fpos) forcing a flush round
+// Ring budget.  A push writes the slot of the incomplete dword, so the settled bytes past fpos
+// must stay <= 4 * ENC_RING - 1.  After a flush round they are <= FLUSH_AT - 1 (whole dwords <
+// FLUSH_AT, plus <= 3 bytes in the incomplete one).  Flush checks come every 8 symbols and after
+// every rare path.  Until the next check, small models on the paired path (ENC_PAIR) settle at
+// most 3 pairs of 3-byte symbols, then one pair whose two symbols both take the rare path (3
+// no-carry bytes + up to 7 range_reduction_expansion bytes each); unpaired (and wide) models
+// at most 7 symbols of <= 3 bytes and one rare symbol (<= 8 no-carry + 7 reduction bytes).
+static_assert(FLUSH_AT % 4 == 0, "FLUSH_AT counts whole dwords");
+static_assert(FLUSH_AT - 1 + 6 * 3 + 2 * (3 + 7) <= 4 * ENC_RING - 1,
+              "paired small-model encoder may overrun its output ring");
+static_assert(FLUSH_AT - 1 + 7 * 3 + (8 + 7) <= 4 * ENC_RING - 1,
+              "unpaired encoder may overrun its output ring");
 #define SINK_SLOTS 65536
 __device__ uint4 g_sink[SINK_SLOTS];  // dummy symbol tiles of dead lanes (contents irrelevant)
 

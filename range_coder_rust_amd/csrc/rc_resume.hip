@@ -248,26 +248,33 @@ struct Dev {
 // on the context's stream.  (Small async copies to and from pageable memory returned wrong
 // bytes intermittently on this stack; pinned staging is also the faster path.)  The block is
 // held under its own mutex for the whole call: the Python mirrors share one default context
-// between threads, and ctypes releases the GIL inside the call.
+// between threads, and ctypes releases the GIL inside the call.  A call keeps its Stage alive
+// by a shared_ptr, so an rc_ctx_destroy racing with it cannot free the mutex under it; the
+// release marks the block dead, and a call that locks it afterwards fails instead of
+// re-growing a block nobody would free.
 struct Stage {
   std::mutex mu;
   char* host = nullptr;
   char* dev = nullptr;
   size_t cap = 0;
+  bool dead = false;
 };
 std::mutex g_stage_mu;
-std::unordered_map<const rc_ctx*, std::unique_ptr<Stage>> g_stages;
+std::unordered_map<const rc_ctx*, std::shared_ptr<Stage>> g_stages;
 
-// Locks the context's block (released when `lk` goes out of scope) and grows it to `bytes`.
-char* stage_acquire(const rc_ctx* ctx, size_t bytes, char** dev, std::unique_lock<std::mutex>* lk) {
-  Stage* st;
+// Locks the context's block (released when `lk` goes out of scope; `keep` holds the block
+// alive until then, so declare it before `lk`) and grows it to `bytes`.
+char* stage_acquire(const rc_ctx* ctx, size_t bytes, char** dev, std::shared_ptr<Stage>* keep,
+                    std::unique_lock<std::mutex>* lk) {
   {
     std::lock_guard<std::mutex> g(g_stage_mu);
     auto& slot = g_stages[ctx];
-    if (!slot) slot.reset(new Stage);
-    st = slot.get();
+    if (!slot) slot = std::make_shared<Stage>();
+    *keep = slot;
   }
+  Stage* st = keep->get();
   *lk = std::unique_lock<std::mutex>(st->mu);
+  if (st->dead) return nullptr;  // the context is being destroyed
   if (st->cap < bytes) {
     if (st->host) (void)hipHostFree(st->host);
     if (st->dev) (void)hipFree(st->dev);
@@ -349,8 +356,9 @@ rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint3
   const size_t o_off = 64, o_len = o_off + 32, o_fl = o_len + 16, o_tr = o_fl + 16;
   const size_t o_nb = o_tr + ((12 * n + 15) & ~15ull), o_out = o_nb + ((n + 15) & ~15ull);
   char* d = nullptr;
+  std::shared_ptr<Stage> keep;
   std::unique_lock<std::mutex> lk;
-  char* h = stage_acquire(ctx, o_out + need, &d, &lk);
+  char* h = stage_acquire(ctx, o_out + need, &d, &keep, &lk);
   if (!h) return RC_E_DEVICE;
   memcpy(h, state, sizeof *state);
   const u64 offs[4] = {0, n, 0, need};  // sym_off[0..1], out_off[0..1]
@@ -417,8 +425,9 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
   const size_t o_off = 64, o_fl = o_off + 32, o_c = o_fl + 16, o_cum = o_c + 1024;
   const size_t o_win = o_cum + 1024, o_sym = o_win + ((wlen + 15) & ~15ull);
   char* d = nullptr;
+  std::shared_ptr<Stage> keep;
   std::unique_lock<std::mutex> lk;
-  char* h = stage_acquire(ctx, o_sym + n, &d, &lk);
+  char* h = stage_acquire(ctx, o_sym + n, &d, &keep, &lk);
   if (!h) return RC_E_DEVICE;
   rc_stream_state rel = *state;
   rel.pos -= p0;  // the window starts at p0 (stage 0: at the stream start)
@@ -455,7 +464,7 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
 
 // internal: free the context's staging block (called by rc_ctx_destroy)
 void rc_resume_release_(const rc_ctx* ctx) {
-  std::unique_ptr<Stage> st;
+  std::shared_ptr<Stage> st;
   {
     std::lock_guard<std::mutex> lk(g_stage_mu);
     auto it = g_stages.find(ctx);
@@ -466,6 +475,9 @@ void rc_resume_release_(const rc_ctx* ctx) {
   std::lock_guard<std::mutex> lk(st->mu);  // a call still inside the block finishes first
   if (st->host) (void)hipHostFree(st->host);
   if (st->dev) (void)hipFree(st->dev);
+  st->host = st->dev = nullptr;
+  st->cap = 0;
+  st->dead = true;
 }
 
 }  // extern "C"

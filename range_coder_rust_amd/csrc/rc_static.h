@@ -53,6 +53,10 @@
 #ifndef DEC_TAB_LDS
 #define DEC_TAB_LDS 1        // direct-LUT decoders: keep the (cum, c) table in LDS too
 #endif
+#ifdef RC_RING_GUARD
+// scratch builds only (not part of the C ABI): a decoder read code bytes its ring had not staged
+#define RC_F_RING_GUARD 0x100u
+#endif
 #define LUT_BITS 12
 #define LUT_MAX_ENTRIES (1u << LUT_BITS)
 #ifndef SM_LUT_BITS
