@@ -27,15 +27,54 @@ typedef u32 u32x3 __attribute__((ext_vector_type(3)));
 #define RC_VGPR_FLOOR_144() asm volatile("; vgpr floor 144" ::: "v143")
 #define RC_VGPR_FLOOR_160() asm volatile("; vgpr floor 160" ::: "v159")
 
-// Scratch builds only ("what binds"): -DRC_FILL=n adds n independent 2-cycle
-// VALU instructions to every symbol step of the static coders.  If the step is bound by VALU
-// issue the kernel slows by about n x 2 cycles per wave-symbol; if it waits on latency, the
-// fillers ride in idle issue slots.
+// Scratch builds only ("what binds"): -DRC_FILL=n adds n filler VALU
+// instructions to every symbol step of the static coders, each dependent only on the previous
+// filler (their register is carried in the coder state).  If the step is bound by VALU issue
+// the kernel slows by n x the filler's issue cost per wave-symbol; if it waits on latency, the
+// fillers ride in idle issue slots.  -DRC_FILL_OP picks the instruction, so the marginal cost
+// of each instruction class can be measured inside the real kernels (tools/fill_cost.sh).
 #ifdef RC_FILL
+#ifndef RC_FILL_OP
+#define RC_FILL_OP 0
+#endif
+// the filler register: a VGPR pair for the 64-bit instructions, one VGPR otherwise
+#if RC_FILL_OP == 2 || RC_FILL_OP == 3 || RC_FILL_OP == 5 || RC_FILL_OP == 8 || RC_FILL_OP == 16
+typedef u64 rc_fill_t;
+#else
+typedef u32 rc_fill_t;
+#endif
+static __device__ __forceinline__ void rc_filler_one(u64& x) {
+  u64 c;
+  switch (RC_FILL_OP) {
+    case 2: asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(x)); break;
+    case 3: asm volatile("v_mad_u64_u32 %0, %1, %2, %2, %0" : "+v"(x), "=s"(c) : "v"((u32)(x >> 7))); break;
+    case 5: asm volatile("v_cmp_gt_u64_e64 %0, %1, %1" : "=s"(c) : "v"(x)); break;
+    case 8: asm volatile("v_lshl_add_u64 %0, %0, 1, %0" : "+v"(x)); break;
+    default: asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(x)); break;
+  }
+}
+static __device__ __forceinline__ void rc_filler_one(u32& x) {
+  u64 c;
+  switch (RC_FILL_OP) {
+    case 0: asm volatile("v_add_u32 %0, 1, %0" : "+v"(x)); break;
+    case 1: asm volatile("v_lshrrev_b32 %0, 1, %0" : "+v"(x)); break;
+    case 4: asm volatile("v_mad_u32_u24 %0, %0, %0, %0" : "+v"(x)); break;
+    case 6: asm volatile("v_alignbit_b32 %0, %0, %0, %0" : "+v"(x)); break;
+    case 7: asm volatile("v_perm_b32 %0, %0, %0, %0" : "+v"(x)); break;
+    case 9: asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(x)); break;
+    case 10: asm volatile("v_bfe_u32 %0, %0, 1, 8" : "+v"(x)); break;
+    case 11: asm volatile("v_lshl_add_u32 %0, %0, 3, %0" : "+v"(x)); break;
+    case 12: asm volatile("v_ffbh_u32 %0, %0" : "+v"(x)); break;
+    case 13: asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(x)); break;
+    case 14: asm volatile("v_cmp_gt_u32_e64 %0, %1, %1" : "=s"(c) : "v"(x)); break;
+    case 15: asm volatile("v_mul_f32 %0, %0, %0" : "+v"(x)); break;
+    default: asm volatile("v_xor_b32 %0, 1, %0" : "+v"(x)); break;
+  }
+}
 #define RC_FILLER(x)                                                   \
   do {                                                                 \
     _Pragma("unroll") for (int i_ = 0; i_ < RC_FILL; ++i_)             \
-        asm volatile("v_add_u32 %0, 1, %0" : "+v"(x));                 \
+        rc_filler_one(x);                                              \
   } while (0)
 #else
 #define RC_FILLER(x) \

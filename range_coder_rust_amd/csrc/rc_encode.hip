@@ -37,7 +37,7 @@ struct Enc {
                    // dword B >> 5 of the stream is the incomplete one (its ring slot is free)
   u32 fpos;        // byte position of the next unit to store
 #ifdef RC_FILL
-  u32 fill;        // scratch builds: the filler instructions' register
+  rc_fill_t fill;  // scratch builds: the filler instructions' register
 #endif
   u32 err;         // first RC_F_* error of this chunk (SM: OR of staged table flags)
   u32 ring;        // LDS byte address of this lane's ring column: dword j at ring + 256 * j.
@@ -178,19 +178,23 @@ static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint
   // (SM: the high halves differ, so clz of a nonzero value, as a builtin: asm would be padded)
   const u32 z = SM ? (u32)__builtin_clz(lh ^ hi32(e.low + e.range)) : ffbh(lh ^ hi32(e.low + e.range));
   const u32 nb = z & 24u;
+#ifndef RC_EXP_NOOUT
   const u32 bytes = __builtin_amdgcn_ubfe(lh, 32u - nb, nb);  // the top nb bits (0 if nb == 0)
   e.acc = (e.acc << nb) | bytes;
+#endif
   e.low <<= nb;
   e.range <<= nb;
   // push: the slot of the dword that was incomplete before this symbol gets the 32 bits above
   // the (new) incomplete ones; if it is still incomplete the slot is rewritten later
   // Slot (B >> 5) & (ENC_RING - 1) sits at byte 256 slot of the column: (B & 0x3E0) << 3, an and
   // plus one v_lshl_add_u32 (written out: the compiler's form is a shift, an and and an add)
+#ifndef RC_EXP_NOOUT  // (scratch builds: the coder's arithmetic alone, output dropped; timing only)
   u32 soff, saddr;
   asm("v_and_b32 %0, %1, %2" : "=v"(soff) : "i"((ENC_RING - 1) << 5), "v"(e.B));
   asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(saddr) : "v"(soff), "v"(e.ring));
   e.B += nb;
   *(__attribute__((address_space(3))) u32*)(uintptr_t)saddr = (u32)(e.acc >> (e.B & 31u));
+#endif
   // SM: range >= 2^32 after narrowing, so the high halves differ (z <= 31) and at most 3 bytes
   // settle; only range_reduction_expansion can be pending
   if (SM) return hi32(e.range) < 0x10000u;

@@ -356,16 +356,30 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
       ent[4 * b + 3] = tcb(s1);
     }
   }
-  // small bucket models (the decoder's SM path) test the hint against s1's absolute cum, one
-  // instruction fewer than its offset inside the bucket
+  // small bucket models (the decoder's LUT 4, rc_static.h): 8-B buckets {16 s0 | 16 s1 << 16,
+  // cum[s1]} (s1's absolute cum; 0 without a split, where s1 = s0), at most 2^SMB_LUT_BITS of
+  // them and at least 8 frequencies each, so the bucket's byte address is (q >> la_shift) &
+  // la_mask with la_shift = lut_shift - 3 >= 0
   if (!a.direct && total_freq <= 65536) {
-    for (size_t b = 0; b < lut.size(); ++b) {
-      const u32 e = lut[b], split = e >> 16;
-      // (padded buckets repeat the last real one, (total - 1) >> lut_shift)
-      const u32 br = (u32)std::min<size_t>(b, (total_freq - 1) >> a.lut_shift);
-      const u32 cum1 = split == 0xFFFFu ? 0u : (br << a.lut_shift) + split;
-      lut[b] = (e & 0xFFFFu) | cum1 << 16;
+    const u32 bits = std::min<u32>(SMB_LUT_BITS, bl - 3);  // (total > 2048: bl >= 12)
+    u32 shift = 0;
+    const std::vector<u32> lt = bucket_lut(bits, &shift);
+    if (shift < 3 || lt.size() != (1u << bits)) return RC_E_BAD_MODEL;  // unreachable
+    std::vector<u32> l8(2 * lt.size());
+    for (size_t b = 0; b < lt.size(); ++b) {
+      const u32 e = lt[b], s0 = e & 255u, s1 = (e >> 8) & 255u, split = e >> 16;
+      // (padded buckets repeat the last real one, (total - 1) >> shift)
+      const u32 br = (u32)std::min<size_t>(b, (total_freq - 1) >> shift);
+      const u32 cum1 = split == 0xFFFFu ? 0u : (br << shift) + split;
+      l8[2 * b] = 16 * s0 | (16 * s1) << 16;
+      l8[2 * b + 1] = cum1;
     }
+    a.lut_bits = bits;
+    a.lut_shift = shift;
+    a.la_shift = shift - 3;
+    a.la_mask = ((u32)lt.size() - 1) << 3;
+    a.lut_max = (u32)lt.size() - 1;
+    lut.swap(l8);
   }
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;

@@ -38,6 +38,9 @@
 #ifndef DEC_LD
 #define DEC_LD 4             // 16-B blocks per global load burst (64 B: two refills)
 #endif
+#ifndef DEC_PAIR512_LD
+#define DEC_PAIR512_LD DEC_LD  // load burst of the 512-lane pair decoder (2 waves/SIMD shapes)
+#endif
 #ifndef DEC_OUT_BURST
 #define DEC_OUT_BURST 4      // 16-B symbol blocks per lane per output burst (4: 64 B)
 #endif
@@ -85,7 +88,18 @@ struct ModelArgs {
   const u32* pair;   // pair-bucket tables (k_decode_static LUT 3; null when the model has none):
                      // PAIR_S_WORDS words of {s0 | s1 << 8} (u16 per bucket), then one 16-B
                      // entry per bucket {cum0 | c0 << 16, cum1 | c1 << 16, total/c0, total/c1}
+  u32 la_shift;      // small bucket models (LUT 4): bucket byte address = (q >> la_shift) & la_mask
+  u32 la_mask;
 };
+
+// Small bucket models (k_decode_static LUT 4: 2048 < total <= 2^16, not pair-decoded).  LDS
+// holds the symbol table at address 0, one 16-B entry {cum, c, total/c as f32, s} per symbol at
+// byte 16 s, then 2^SMB_LUT_BITS 8-B buckets {16 s0 | 16 s1 << 16, cum[s1]} at SMB_LUT_OFF: the
+// candidate's table address is one v_perm_b32 of its bucket entry, with no shift or bit-field
+// extract, and the candidate's whole entry one ds_read_b128.
+#define SMB_LUT_BITS 11u
+#define SMB_TAB_WORDS 1024u                      // the symbol table
+#define SMB_LUT_OFF (SMB_TAB_WORDS * 4)          // bytes
 
 // Pair-bucket decoding (LUT 3): models with 2^15 < total <= 2^16 (buckets of 16 frequencies) and
 // every c < 2^16.  A bucket's entry holds both candidates of its bucket table entry, so the
