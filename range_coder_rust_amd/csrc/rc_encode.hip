@@ -2,10 +2,6 @@
 // notes shared with the decoder).
 #include "rc_static.h"
 
-#include <stdlib.h>
-
-#include <atomic>
-
 // ------------------------------------------------------------------------------------------
 // Encoder
 //
@@ -450,349 +446,13 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
 }
 
 
-// ------------------------------------------------------------------------------------------
-// Split encoder, for launches too small to fill the chip (the configs[4] shard of 2^17 chunks
-// at N = 8 gives k_encode_static 2 waves per SIMD, where its per-symbol dependency chain, not
-// issue, sets the rate).  Per 64 chunks, two waves:
-//  * the coder wave runs param_update for its 64 chunks and nothing else: per symbol it hands the
-//    output wave {hi32(L), T}, L = lower_bound + r * cum before the renormalisation and T the
-//    bits the symbol settles (8 per byte; no_carry_expansion and range_reduction_expansion both
-//    emit the top bytes of L, then zeros, so L and T say every byte), plus lo32(L) when T > 24;
-//  * the output wave stages the coder's input symbols (any alignment, 16 B per lane per 16
-//    symbols, through a two-stage select + v_alignbyte funnel) and turns the {L, T} entries into
-//    bytes through the same ring and cooperative flush rounds as k_encode_static.
-// The two meet in an LDS FIFO of two SPL_H-symbol halves, one barrier per half.  A wave pair per
-// 64 chunks doubles the waves per SIMD at this shape, and the coder wave's issue slots all go to
-// the dependency chain.  Encoder::finish is three entries (24 + 24 + 16 bits of
-// the final lower_bound), so every entry's T fits the common path's 24-bit field.
-// ------------------------------------------------------------------------------------------
-#define SPL_H 4  // symbols per FIFO half
-
-template <int DIV, int SM>
-struct SplCoder {
-  u64 low, range;
-  u32 err;
-};
-
-// param_update (range_coder.rs:53-92) up to the closed-form no_carry_expansion: returns L (the
-// lower bound before the shift) and sets nb; the state is left shifted by nb.  True when the lane
-// needs the rest of the expansions (SplCoder::rare).
-template <int DIV, int SM>
-static __device__ __forceinline__ bool spl_step(SplCoder<DIV, SM>& e, const ModelArgs& m,
-                                                uint2 t, u64& L, u32& nb) {
-  u32 c, cum;
-  if (SM == 2) {
-    cum = t.x;
-    c = t.y;
-  } else if (SM) {
-    asm volatile("v_or_b32 %0, %0, %1" : "+v"(e.err) : "v"(t.x));
-    cum = t.x & 0xFFFFFFu;
-    c = t.y;
-  } else {
-    const bool bad = t.y == 0;
-    const u32 code = t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ;
-    e.err = (bad && e.err == 0) ? code : e.err;
-    c = bad ? 1u : t.y;
-    cum = bad ? 0u : t.x;
-  }
-  const u64 r = range_par_total<DIV>(e.range, m);
-  u64 R;
-  if (SM) {
-    const u32 rl = (u32)r, rh = hi32(r);
-    const u64 R0 = (u64)rl * c;
-    const u64 L0 = (u64)rl * cum + e.low;
-    R = ((u64)(hi32(R0) + __umul24(rh, c)) << 32) | (u32)R0;
-    L = ((u64)(hi32(L0) + __umul24(rh, cum)) << 32) | (u32)L0;
-  } else {
-    R = r * (u64)c;
-    L = e.low + r * (u64)cum;
-  }
-  const u32 lh = hi32(L);
-  const u32 z = SM ? (u32)__builtin_clz(lh ^ hi32(L + R)) : ffbh(lh ^ hi32(L + R));
-  nb = z & 24u;
-  e.low = L << nb;
-  e.range = R << nb;
-  if (SM) return hi32(e.range) < 0x10000u;
-  return (z > 31u) | (hi32(e.range) < 0x10000u);
-}
-
-// the rest of a rare symbol: no_carry_expansion past 3 bytes (range_coder.rs:110-116) and
-// range_reduction_expansion (:126-135); t: bits settled so far, returned with theirs added
-template <int DIV, int SM>
-static __device__ __forceinline__ u32 spl_rare(SplCoder<DIV, SM>& e, u32 t) {
-  while (((e.low ^ (e.low + e.range)) >> 56) == 0) {
-    e.low <<= 8;
-    e.range <<= 8;
-    t += 8;
-  }
-  while (e.range < TOP16) {
-    e.range = ~e.low & (TOP16 - 1);
-    e.low <<= 8;
-    e.range <<= 8;
-    t += 8;
-  }
-  return t;
-}
-
-// the output wave: T bits from the top of L into the accumulator and the ring (T <= 24)
-static __device__ __forceinline__ void spl_emit(Enc& e, u32 lh, u32 t) {
-  const u32 bytes = __builtin_amdgcn_ubfe(lh, 32u - t, t);  // (t = 0: width 0, nothing)
-  e.acc = (e.acc << t) | bytes;
-  u32 soff, saddr;
-  asm("v_and_b32 %0, %1, %2" : "=v"(soff) : "i"((ENC_RING - 1) << 5), "v"(e.B));
-  asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(saddr) : "v"(soff), "v"(e.ring));
-  e.B += t;
-  *(__attribute__((address_space(3))) u32*)(uintptr_t)saddr = (u32)(e.acc >> (e.B & 31u));
-}
-
-template <int DIV, int SM>
-__global__ __launch_bounds__(128, 8) void k_encode_split(ModelArgs m, const uint8_t* __restrict__ syms,
-                                                      const u64* __restrict__ sym_off,
-                                                      u32 n_chunks, uint8_t* __restrict__ out,
-                                                      const u64* __restrict__ out_off,
-                                                      u64* __restrict__ out_len,
-                                                      u32* __restrict__ flags) {
-  __shared__ uint2 s_tab[256];
-  __shared__ uint4 s_in[2][64];           // staged symbols: 16 per lane per block
-  __shared__ uint2 s_fifo[2][SPL_H][64];  // {hi32(L), T}
-  __shared__ u32 s_fifo_lo[2][SPL_H][64]; // lo32(L), written when T > 24
-  __shared__ u32 s_ring[ENC_RING * 64];
-  __shared__ EncOut s_out[64];
-  __shared__ u32 s_err[64];
-  const u32 tid = threadIdx.x, lane = tid & 63;
-  const bool coder = tid < 64;  // wave 0: coder, wave 1: output
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    uint2 t = m.tab[tid + 128 * q];
-    if (SM == 1 && t.y == 0)
-      t = make_uint2((t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ) << 24, 1u);
-    s_tab[tid + 128 * q] = t;
-  }
-  const u32 k = blockIdx.x * 64 + lane;
-  const bool live = k < n_chunks;
-  u64 s0 = 0, n = 0, o0 = 0, o1 = 0;
-  if (live) {
-    s0 = sym_off[k];
-    n = sym_off[k + 1] - s0;
-    o0 = out_off[k];
-    o1 = out_off[k + 1];
-  }
-  const bool too_long = n > RC_MAX_CHUNK_SYMBOLS;
-  if (too_long) {
-    n = 0;
-    o1 = o0;
-  }
-  const u32 n32 = (u32)n;
-  // wave-uniform symbol range: every lane's n, then its three finish entries
-  u32 nmax = n32, nmin = live ? n32 : ~0u;
-#pragma unroll
-  for (int o = 32; o; o >>= 1) {
-    nmax = max(nmax, (u32)__shfl_xor((int)nmax, o));
-    nmin = min(nmin, (u32)__shfl_xor((int)nmin, o));
-  }
-  nmax = __builtin_amdgcn_readfirstlane(nmax);
-  nmin = __builtin_amdgcn_readfirstlane(nmin == ~0u ? 0u : nmin);
-  const u32 nh = (nmax + 3 + SPL_H - 1) / SPL_H;  // FIFO halves
-  const uint8_t* sp = syms + s0;
-
-  if (coder) {
-    SplCoder<DIV, SM> e;
-    e.low = 0;
-    e.range = ~0ull;
-    e.err = 0;
-    __syncthreads();  // block 0 staged
-    for (u32 h4 = 0; h4 < nh; h4 += 4) {  // one staged block (16 symbols) per trip
-      const uint4 blk = s_in[(h4 >> 2) & 1][lane];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-      const u32 h = h4 + q;
-      if (h >= nh) break;
-      const u32 w = q == 0 ? blk.x : q == 1 ? blk.y : q == 2 ? blk.z : blk.w;
-      uint2* fe = s_fifo[h & 1][0] + lane;
-      u32* fl = s_fifo_lo[h & 1][0] + lane;
-      const u32 i0 = h * SPL_H;
-      if (i0 + SPL_H <= nmin) {
-        // every lane codes all four symbols: two pairs, one rare test each (as enc_sym2)
-#pragma unroll
-        for (int j = 0; j < SPL_H; j += 2) {
-          const uint2 t0 = s_tab[(w >> (8 * j)) & 255u], t1 = s_tab[(w >> (8 * j + 8)) & 255u];
-          u64 L0, L1;
-          u32 b0, b1;
-          const bool r0 = spl_step<DIV, SM>(e, m, t0, L0, b0);
-          const SplCoder<DIV, SM> ea = e;
-          bool r1 = spl_step<DIV, SM>(e, m, t1, L1, b1);
-          if (__builtin_expect(__any((int)(r0 | r1)), 0)) {
-            if (r0) {
-              e = ea;
-              b0 = spl_rare(e, b0);
-              r1 = spl_step<DIV, SM>(e, m, t1, L1, b1);
-            }
-            if (r1) b1 = spl_rare(e, b1);
-            if (b0 > 24) fl[64 * j] = (u32)L0;
-            if (b1 > 24) fl[64 * (j + 1)] = (u32)L1;
-          }
-          fe[64 * j] = make_uint2(hi32(L0), b0);
-          fe[64 * (j + 1)] = make_uint2(hi32(L1), b1);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < SPL_H; ++j) {
-          const u32 i = i0 + j;
-          uint2 en = make_uint2(0u, 0u);
-          if (i < n32) {
-            u64 L;
-            u32 b;
-            if (spl_step<DIV, SM>(e, m, s_tab[(w >> (8 * j)) & 255u], L, b)) {
-              b = spl_rare(e, b);
-              fl[64 * j] = (u32)L;
-            }
-            en = make_uint2(hi32(L), b);
-          } else if (i < n32 + 3) {  // Encoder::finish (encoder.rs:40-46): the 8 bytes of low
-            const u32 f = i - n32;
-            en = make_uint2(hi32(e.low << (24 * f)), f < 2 ? 24u : 16u);
-          }
-          fe[64 * j] = en;
-        }
-      }
-      __syncthreads();
-      }
-    }
-    if (live) {
-      if (SM == 1) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
-      s_err[lane] = e.err;
-    }
-    __syncthreads();
-    return;
-  }
-
-  // ---- output wave ----
-  const u32 a = (u32)(((uintptr_t)out + o0) & (ENC_UNIT - 1));
-  u64 cap = o1 - o0;
-  if (cap > 0xFFFFFF00ull - a) cap = 0xFFFFFF00ull - a;
-  s_out[lane].gbase = out + o0 - a;
-  s_out[lane].lo_ok = a;
-  s_out[lane].hi_ok = a + (u32)cap;
-  Enc e;
-#ifdef RC_FILL
-  e.fill = 0;
-#endif
-  e.low = 0;
-  e.range = 0;
-  e.acc = 0;
-  e.B = 8 * a;
-  e.fpos = 0;
-  e.err = 0;
-  e.ring = (u32)(uintptr_t)(__attribute__((address_space(3))) u32*)(s_ring + lane);
-  const u32* wring = s_ring;
-  const EncOut* wout = s_out;
-  // input staging: 16-B aligned loads of the lane's stream (clamped to its last block), shifted
-  // by the stream's offset o in two selects of dwords and one v_alignbyte_b32
-  const u32 o = (u32)((uintptr_t)sp & 15);
-  const bool has_in = live && n > 0;
-  const uint4* ab = has_in ? reinterpret_cast<const uint4*>(sp - o)
-                           : reinterpret_cast<const uint4*>(g_sink);
-  const u32 glast = has_in ? (u32)((o + n - 1) >> 4) : 0u;
-  const u32 m2 = (o & 8) ? ~0u : 0u, m1 = (o & 4) ? ~0u : 0u;
-  uint4 ax = ab[0];
-  auto stage = [&](u32 b) {  // symbols [16 b, 16 b + 16) into s_in[b & 1]
-    const uint4 ay = ab[min(b + 1, glast)];
-    const u32 W[8] = {ax.x, ax.y, ax.z, ax.w, ay.x, ay.y, ay.z, ay.w};
-    u32 V[6], U[5];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) V[i] = mselc(m2, W[i + 2], W[i]);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) U[i] = mselc(m1, V[i + 1], V[i]);
-    s_in[b & 1][lane] = make_uint4(__builtin_amdgcn_alignbyte(U[1], U[0], o),
-                                   __builtin_amdgcn_alignbyte(U[2], U[1], o),
-                                   __builtin_amdgcn_alignbyte(U[3], U[2], o),
-                                   __builtin_amdgcn_alignbyte(U[4], U[3], o));
-    ax = ay;
-  };
-  stage(0);
-  __syncthreads();
-  auto consume = [&](u32 hp) {
-    const uint2* fe = s_fifo[hp & 1][0] + lane;
-    const u32* fl = s_fifo_lo[hp & 1][0] + lane;
-#pragma unroll
-    for (int j = 0; j < SPL_H; ++j) {
-      const uint2 en = fe[64 * j];
-      if (__builtin_expect(__any((int)(en.y > 24u)), 0)) {
-        if (en.y > 24u) {  // a rare symbol: its bytes one by one from the top of L, then zeros
-          u64 L = ((u64)en.x << 32) | fl[64 * j];
-          for (u32 t = 0; t < en.y; t += 8) {
-            enc_emit_byte(e, (u32)(L >> 56));
-            L <<= 8;
-          }
-        } else {
-          spl_emit(e, en.x, en.y);
-        }
-        enc_flush(e, lane, wring, wout);
-      } else {
-        spl_emit(e, en.x, en.y);
-      }
-    }
-    enc_flush(e, lane, wring, wout);
-  };
-  for (u32 h = 0; h < nh; ++h) {
-    if ((h & 3) == 0) stage((h >> 2) + 1);
-    if (h) consume(h - 1);
-    __syncthreads();
-  }
-  if (nh) consume(nh - 1);
-  const u32 len = (e.B >> 3) - a;
-  u32 wend = enc_wpos(e);
-  if (e.B & 31) {
-    ring_put(e.ring, (e.B >> 5) & (ENC_RING - 1), (u32)(e.acc << (32 - (e.B & 31))));
-    wend += 4;
-  }
-  const u32 end = a + len;
-  if (end < s_out[lane].hi_ok) s_out[lane].hi_ok = end;
-  while (__any((int)(e.fpos < wend))) enc_round(e, e.fpos < wend, lane, wring, wout);
-  __syncthreads();  // the coder's flags
-  if (live) {
-    u32 err = s_err[lane];
-    if (!err && (u64)len > cap) err = RC_F_CAPACITY;
-    out_len[k] = too_long ? 0u : len;
-    flags[k] = too_long ? RC_F_TOO_LONG : err;
-  }
-}
-
-namespace {
-// Split encoder for a launch (RC_ENC_SPLIT=0 / 1 overrides; read at every launch, as tests
-// switch it): when the chunks give k_encode_static at most 2 waves per SIMD
-bool use_split(u32 n_chunks) {
-  const char* e = getenv("RC_ENC_SPLIT");
-  if (e && *e) return strtol(e, nullptr, 10) != 0;
-  static std::atomic<u32> cache[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return false;
-  u32 cus = dev < 64 ? cache[dev].load(std::memory_order_relaxed) : 0u;
-  if (!cus) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        v <= 0)
-      v = 256;
-    cus = (u32)v;
-    if (dev < 64) cache[dev].store(cus, std::memory_order_relaxed);
-  }
-  return (u64)n_chunks <= (u64)cus * 512;
-}
-}  // namespace
-
 hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a, int div, int smv,
                                    const uint8_t* syms, const u64* sym_off, u32 n_chunks,
                                    uint8_t* out, const u64* out_off, u64* out_len, u32* flags) {
-  const bool split = use_split(n_chunks);
-  const dim3 grid(split ? (n_chunks + 63) / 64 : (n_chunks + WG - 1) / WG), block(split ? 128 : WG);
+  const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
 #define RC_ENC_LAUNCH(D, S)                                                                   \
-  do {                                                                                        \
-    if (split)                                                                                \
-      hipLaunchKernelGGL((k_encode_split<D, S>), grid, block, 0, stream, a, syms, sym_off,   \
-                         n_chunks, out, out_off, out_len, flags);                             \
-    else                                                                                      \
-      hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, stream, a, syms, sym_off,  \
-                         n_chunks, out, out_off, out_len, flags);                             \
-  } while (0)
+  hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, stream, a, syms, sym_off,      \
+                     n_chunks, out, out_off, out_len, flags)
 #ifdef RC_DEV_ONLY  // scratch builds for kernel tuning: the headline variants only
   if (div != DIV_POW2 || smv == 0) return hipErrorInvalidValue;
   if (smv == 2) RC_ENC_LAUNCH(DIV_POW2, 2); else RC_ENC_LAUNCH(DIV_POW2, 1);

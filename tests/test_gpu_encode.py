@@ -1,11 +1,10 @@
-"""Both static encoders on the same streams: k_encode_static (one wave per 64 chunks) and
-k_encode_split (a coder wave and an output wave per 64 chunks, the low-occupancy launches;
-rc_encode.hip).  RC_ENC_SPLIT=0 / 1 forces the choice; the default picks the split encoder for
-launches of at most CUs x 512 chunks, which is every small test in the suite, so this file is
-what keeps k_encode_static covered at small sizes.  Bytes, lengths and flags against the oracle
-for every model class (wide, small, small and complete; power-of-two and magic totals), ragged
-and misaligned chunks, rare-heavy streams (range_reduction_expansion back to back), the
-reference's errors, capacity overflow, and the directed ring fixtures."""
+"""k_encode_static (rc_encode.hip) against the oracle, one battery per model class: wide, small,
+small and complete; power-of-two and magic totals; the headline uniform model and a rare-heavy
+one (range_reduction_expansion back to back).  Ragged and misaligned chunks, the reference's
+errors (the first one wins), capacity overflow (the exact length, nothing written past the
+slot), and the decoder's directed ring fixtures, whose streams the encoder must reproduce.
+(Round 4 ran the same battery on a split coder-wave / output-wave encoder before measuring it
+slower)"""
 import json
 import os
 
@@ -54,10 +53,8 @@ def _models(rng):
     return out
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("misalign", [False, True])
-def test_encoders_vs_oracle(ctx, monkeypatch, split, misalign):
-    monkeypatch.setenv("RC_ENC_SPLIT", split)
+def test_encoder_vs_oracle(ctx, misalign):
     rng = np.random.default_rng(5 + misalign)
     for name, c in _models(rng):
         cum = cum_of(c)
@@ -79,15 +76,13 @@ def test_encoders_vs_oracle(ctx, monkeypatch, split, misalign):
         out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=misalign, seed=len(name))
         for k, ch in enumerate(chunks):
             f, b, L = cpu.encode(c, cum, total, ch)
-            assert (fl[k], ol[k]) == (f, L), (name, split, k, fl[k], f, ol[k], L)
-            assert bytes(out[out_off[k]: out_off[k] + ol[k]]) == b, (name, split, k)
+            assert (fl[k], ol[k]) == (f, L), (name, k, fl[k], f, ol[k], L)
+            assert bytes(out[out_off[k]: out_off[k] + ol[k]]) == b, (name, k)
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_encoders_errors_and_capacity(ctx, monkeypatch, split):
+def test_encoder_errors_and_capacity(ctx):
     """Zero-frequency and out-of-alphabet symbols (the first error wins) and slots too small for
     the stream (RC_F_CAPACITY with the exact length, nothing written past the slot)."""
-    monkeypatch.setenv("RC_ENC_SPLIT", split)
     rng = np.random.default_rng(17)
     for total_kind in ("small", "wide"):
         if total_kind == "small":
@@ -117,18 +112,16 @@ def test_encoders_errors_and_capacity(ctx, monkeypatch, split):
             f, want, L = cpu.encode(c, cum, total, ch)
             if f == 0 and L > caps[k]:
                 f = rc.api.N.F_CAPACITY
-            assert fl[k] == f, (total_kind, split, k, fl[k], f)
+            assert fl[k] == f, (total_kind, k, fl[k], f)
             if f in (0, rc.api.N.F_CAPACITY):  # the exact length either way
-                assert ol[k] == L, (total_kind, split, k)
+                assert ol[k] == L, (total_kind, k)
             if f == 0:
-                assert bytes(out[out_off[k]:out_off[k] + L]) == want, (total_kind, split, k)
+                assert bytes(out[out_off[k]:out_off[k] + L]) == want, (total_kind, k)
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_encoders_on_ring_fixtures(ctx, monkeypatch, split):
+def test_encoder_on_ring_fixtures(ctx):
     """The decoder's directed ring fixtures (rare paths at every span offset, 3-byte symbols
     after them) encode to their recorded streams."""
-    monkeypatch.setenv("RC_ENC_SPLIT", split)
     with open(os.path.join(HERE, "golden", "ring_fixtures.json")) as f:
         fx = json.load(f)
     c = np.array(fx["c"], np.uint32)
@@ -138,5 +131,5 @@ def test_encoders_on_ring_fixtures(ctx, monkeypatch, split):
     out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=True, seed=9)
     for k in range(len(chunks)):
         want = bytes.fromhex(fx["chunks"][k % len(fx["chunks"])]["encoded_hex"])
-        assert fl[k] == 0 and ol[k] == len(want), (split, k)
-        assert bytes(out[out_off[k]:out_off[k] + ol[k]]) == want, (split, k)
+        assert fl[k] == 0 and ol[k] == len(want), k
+        assert bytes(out[out_off[k]:out_off[k] + ol[k]]) == want, k
