@@ -133,14 +133,33 @@ static __device__ __forceinline__ void enc_rare(Enc& e) {
   }
 }
 
+// the output of one symbol: its nb settled bits, the top nb bits of lh (hi32 of the lower bound
+// before the shift), into the accumulator and pushed to the ring: the slot of the dword that
+// was incomplete before the symbol gets the 32 bits above the (new) incomplete ones; if it is
+// still incomplete the slot is rewritten later.  Slot (B >> 5) & (ENC_RING - 1) sits at byte
+// 256 slot of the column: (B & 0x3E0) << 3, an and plus one v_lshl_add_u32 (written out: the
+// compiler's form is a shift, an and and an add)
+static __device__ __forceinline__ void enc_out(Enc& e, u32 lh, u32 nb) {
+#ifndef RC_EXP_NOOUT  // (scratch builds: the coder's arithmetic alone, output dropped; timing only)
+  const u32 bytes = __builtin_amdgcn_ubfe(lh, 32u - nb, nb);  // the top nb bits (0 if nb == 0)
+  e.acc = (e.acc << nb) | bytes;
+  u32 soff, saddr;
+  asm("v_and_b32 %0, %1, %2" : "=v"(soff) : "i"((ENC_RING - 1) << 5), "v"(e.B));
+  asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(saddr) : "v"(soff), "v"(e.ring));
+  e.B += nb;
+  *(__attribute__((address_space(3))) u32*)(uintptr_t)saddr = (u32)(e.acc >> (e.B & 31u));
+#endif
+}
+
 // Encoder::encode (encoder.rs:24-37) -> RangeCoder::param_update (range_coder.rs:53-92),
-// common path without branches.  Returns true when the lane needs enc_rare().  Written for the
-// gfx950 VALU price list (profiles/r01/ubench_valu.txt): 64-bit ops, multiplies, compares and
-// bit-field ops cost ~3.6 cycles per wave, plain 32-bit add/logic/right-shift ~2.
+// common path without branches, up to the closed-form no_carry_expansion: sets lh (hi32 of the
+// lower bound before the shift) and nb (the bits that settle), shifts the state, and returns
+// true when the lane needs enc_rare() (after enc_out of this symbol).
 // SM: 0 wide model; 1 small model (256 <= total <= 2^16) that may hold entries the reference
 // cannot encode; 2 small and complete (256 symbols, every c > 0: nothing to check)
 template <int DIV, int SM>
-static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint2 t) {
+static __device__ __forceinline__ bool enc_core(Enc& e, const ModelArgs& m, uint2 t, u32& lh_out,
+                                                u32& nb_out) {
 #ifdef RC_FILL
   RC_FILLER(e.fill);
 #endif
@@ -178,27 +197,23 @@ static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint
   // (SM: the high halves differ, so clz of a nonzero value, as a builtin: asm would be padded)
   const u32 z = SM ? (u32)__builtin_clz(lh ^ hi32(e.low + e.range)) : ffbh(lh ^ hi32(e.low + e.range));
   const u32 nb = z & 24u;
-#ifndef RC_EXP_NOOUT
-  const u32 bytes = __builtin_amdgcn_ubfe(lh, 32u - nb, nb);  // the top nb bits (0 if nb == 0)
-  e.acc = (e.acc << nb) | bytes;
-#endif
   e.low <<= nb;
   e.range <<= nb;
-  // push: the slot of the dword that was incomplete before this symbol gets the 32 bits above
-  // the (new) incomplete ones; if it is still incomplete the slot is rewritten later
-  // Slot (B >> 5) & (ENC_RING - 1) sits at byte 256 slot of the column: (B & 0x3E0) << 3, an and
-  // plus one v_lshl_add_u32 (written out: the compiler's form is a shift, an and and an add)
-#ifndef RC_EXP_NOOUT  // (scratch builds: the coder's arithmetic alone, output dropped; timing only)
-  u32 soff, saddr;
-  asm("v_and_b32 %0, %1, %2" : "=v"(soff) : "i"((ENC_RING - 1) << 5), "v"(e.B));
-  asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(saddr) : "v"(soff), "v"(e.ring));
-  e.B += nb;
-  *(__attribute__((address_space(3))) u32*)(uintptr_t)saddr = (u32)(e.acc >> (e.B & 31u));
-#endif
+  lh_out = lh;
+  nb_out = nb;
   // SM: range >= 2^32 after narrowing, so the high halves differ (z <= 31) and at most 3 bytes
   // settle; only range_reduction_expansion can be pending
   if (SM) return hi32(e.range) < 0x10000u;
   return (z > 31u) | (hi32(e.range) < 0x10000u);
+}
+
+// one symbol, output included
+template <int DIV, int SM>
+static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint2 t) {
+  u32 lh, nb;
+  const bool rare = enc_core<DIV, SM>(e, m, t, lh, nb);
+  enc_out(e, lh, nb);
+  return rare;
 }
 
 // one symbol (table entry t) for the lanes with `act`; the rare path (wave-uniform branch) may

@@ -64,7 +64,7 @@ def trace_ms(d):
 
 def summarise(root):
     out = {}
-    for cfg in ("uniform", "zipf"):
+    for cfg in ("uniform", "zipf", "shard"):
         d = os.path.join(root, cfg)
         if not os.path.isdir(d):
             continue

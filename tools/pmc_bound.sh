@@ -1,8 +1,9 @@
 #!/bin/bash
 # What binds the static kernels: per configuration (uniform: direct-table
 # decoder; zipf: bucket decoder) one kernel-trace pass (durations, VGPR counts) and two SQ counter
-# passes with the GRBM clock counters, over one launch of each kernel at 2^20 x 64 KiB.
-# Usage on the GPU box:  bash tools/pmc_bound.sh TAG   -> gpurun_out/bound_<TAG>/
+# passes with the GRBM clock counters, over one launch of each kernel at 2^20 x 64 KiB; "shard":
+# the configs[4] N = 8 shard (2^17 Zipf chunks: the pair decoder, 2 waves per SIMD).
+# Usage on the GPU box:  [CONFIGS="shard"] bash tools/pmc_bound.sh TAG   -> gpurun_out/bound_<TAG>/
 # then locally: python3 tools/pmc_bound.py gpurun_out/bound_<TAG>
 set -euo pipefail
 TAG=${1:?usage: pmc_bound.sh TAG}
@@ -13,8 +14,12 @@ cd /tmp && export TMPDIR=/tmp
 cd "$ROOT"
 ONE=(--no-cpu-baseline --no-zipf --no-adaptive --no-model-build --no-container --no-host-stream
      --steps 1 --warmup 0)
-for cfg in uniform zipf; do
-  RUN=(python3 bench.py --config $cfg "${ONE[@]}")
+for cfg in ${CONFIGS:-uniform zipf}; do
+  if [ "$cfg" = shard ]; then
+    RUN=(python3 bench.py --config zipf --global-chunks 131072 "${ONE[@]}")
+  else
+    RUN=(python3 bench.py --config $cfg "${ONE[@]}")
+  fi
   mkdir -p "$O/$cfg"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/$cfg/trace" -o run --output-format csv \
     -- "${RUN[@]}" > "$O/$cfg/trace.log" 2>&1
