@@ -2,10 +2,6 @@
 // notes shared with the decoder).
 #include "rc_static.h"
 
-#include <stdlib.h>
-
-#include <atomic>
-
 // ------------------------------------------------------------------------------------------
 // Encoder
 //
@@ -465,364 +461,13 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
 }
 
 
-// ------------------------------------------------------------------------------------------
-// Scratch (-DRC_ENC_SPLIT2): the split encoder with a decoupled FIFO.  A coder wave and an output
-// wave per 64 chunks as k_encode_split of d2b0b96, but the two meet in an 8-symbol LDS FIFO with
-// produced / consumed counters (release / acquire fences, the waiting wave sleeping) instead of a
-// barrier per half, and the coder loads its own input (16-B aligned loads and the select +
-// v_alignbyte funnel), so the waves drift up to 8 symbols apart.  Timing experiment: the
-// default build does not contain it.
-// ------------------------------------------------------------------------------------------
-#ifdef RC_ENC_SPLIT2
-
-template <int DIV, int SM>
-struct SplCoder {
-  u64 low, range;
-  u32 err;
-};
-
-// param_update (range_coder.rs:53-92) up to the closed-form no_carry_expansion: returns L (the
-// lower bound before the shift) and sets nb; the state is left shifted by nb.  True when the lane
-// needs the rest of the expansions (SplCoder::rare).
-template <int DIV, int SM>
-static __device__ __forceinline__ bool spl_step(SplCoder<DIV, SM>& e, const ModelArgs& m,
-                                                uint2 t, u64& L, u32& nb) {
-  u32 c, cum;
-  if (SM == 2) {
-    cum = t.x;
-    c = t.y;
-  } else if (SM) {
-    asm volatile("v_or_b32 %0, %0, %1" : "+v"(e.err) : "v"(t.x));
-    cum = t.x & 0xFFFFFFu;
-    c = t.y;
-  } else {
-    const bool bad = t.y == 0;
-    const u32 code = t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ;
-    e.err = (bad && e.err == 0) ? code : e.err;
-    c = bad ? 1u : t.y;
-    cum = bad ? 0u : t.x;
-  }
-  const u64 r = range_par_total<DIV>(e.range, m);
-  u64 R;
-  if (SM) {
-    const u32 rl = (u32)r, rh = hi32(r);
-    const u64 R0 = (u64)rl * c;
-    const u64 L0 = (u64)rl * cum + e.low;
-    R = ((u64)(hi32(R0) + __umul24(rh, c)) << 32) | (u32)R0;
-    L = ((u64)(hi32(L0) + __umul24(rh, cum)) << 32) | (u32)L0;
-  } else {
-    R = r * (u64)c;
-    L = e.low + r * (u64)cum;
-  }
-  const u32 lh = hi32(L);
-  const u32 z = SM ? (u32)__builtin_clz(lh ^ hi32(L + R)) : ffbh(lh ^ hi32(L + R));
-  nb = z & 24u;
-  e.low = L << nb;
-  e.range = R << nb;
-  if (SM) return hi32(e.range) < 0x10000u;
-  return (z > 31u) | (hi32(e.range) < 0x10000u);
-}
-
-// the rest of a rare symbol: no_carry_expansion past 3 bytes (range_coder.rs:110-116) and
-// range_reduction_expansion (:126-135); t: bits settled so far, returned with theirs added
-template <int DIV, int SM>
-static __device__ __forceinline__ u32 spl_rare(SplCoder<DIV, SM>& e, u32 t) {
-  while (((e.low ^ (e.low + e.range)) >> 56) == 0) {
-    e.low <<= 8;
-    e.range <<= 8;
-    t += 8;
-  }
-  while (e.range < TOP16) {
-    e.range = ~e.low & (TOP16 - 1);
-    e.low <<= 8;
-    e.range <<= 8;
-    t += 8;
-  }
-  return t;
-}
-
-// the output wave: T bits from the top of L into the accumulator and the ring (T <= 24)
-static __device__ __forceinline__ void spl_emit(Enc& e, u32 lh, u32 t) {
-  const u32 bytes = __builtin_amdgcn_ubfe(lh, 32u - t, t);  // (t = 0: width 0, nothing)
-  e.acc = (e.acc << t) | bytes;
-  u32 soff, saddr;
-  asm("v_and_b32 %0, %1, %2" : "=v"(soff) : "i"((ENC_RING - 1) << 5), "v"(e.B));
-  asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(saddr) : "v"(soff), "v"(e.ring));
-  e.B += t;
-  *(__attribute__((address_space(3))) u32*)(uintptr_t)saddr = (u32)(e.acc >> (e.B & 31u));
-}
-
-#define SPL_F 8  // FIFO slots (symbols)
-
-static __device__ __forceinline__ u32 lds_acquire(const volatile u32* p) {
-  const u32 v = *p;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  return __builtin_amdgcn_readfirstlane(v);
-}
-static __device__ __forceinline__ void lds_release(volatile u32* p, u32 v) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  *p = v;
-}
-#define SPL_SPIN_MAX (1u << 24)  // a wait that long means a bug: give up rather than hang
-
-template <int DIV, int SM>
-__global__ __launch_bounds__(128, 8) void k_encode_split(ModelArgs m, const uint8_t* __restrict__ syms,
-                                                      const u64* __restrict__ sym_off,
-                                                      u32 n_chunks, uint8_t* __restrict__ out,
-                                                      const u64* __restrict__ out_off,
-                                                      u64* __restrict__ out_len,
-                                                      u32* __restrict__ flags) {
-  __shared__ uint2 s_tab[256];
-  __shared__ uint2 s_fifo[SPL_F][64];  // {hi32(L), T}
-  __shared__ u32 s_fifo_lo[SPL_F][64];  // lo32(L), written when T > 24
-  __shared__ u32 s_ring[ENC_RING * 64];
-  __shared__ EncOut s_out[64];
-  __shared__ u32 s_err[64];
-  __shared__ u32 s_prod, s_cons;  // entries written by the coder / read by the output wave
-  const u32 tid = threadIdx.x, lane = tid & 63;
-  const bool coder = tid < 64;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    uint2 t = m.tab[tid + 128 * q];
-    if (SM == 1 && t.y == 0)
-      t = make_uint2((t.x == 0xFFFFFFFFu ? RC_F_BAD_SYMBOL : RC_F_ZERO_FREQ) << 24, 1u);
-    s_tab[tid + 128 * q] = t;
-  }
-  if (tid == 0) {
-    s_prod = 0;
-    s_cons = 0;
-  }
-  const u32 k = blockIdx.x * 64 + lane;
-  const bool live = k < n_chunks;
-  u64 s0 = 0, n = 0, o0 = 0, o1 = 0;
-  if (live) {
-    s0 = sym_off[k];
-    n = sym_off[k + 1] - s0;
-    o0 = out_off[k];
-    o1 = out_off[k + 1];
-  }
-  const bool too_long = n > RC_MAX_CHUNK_SYMBOLS;
-  if (too_long) {
-    n = 0;
-    o1 = o0;
-  }
-  const u32 n32 = (u32)n;
-  u32 nmax = n32, nmin = live ? n32 : ~0u;
-#pragma unroll
-  for (int o = 32; o; o >>= 1) {
-    nmax = max(nmax, (u32)__shfl_xor((int)nmax, o));
-    nmin = min(nmin, (u32)__shfl_xor((int)nmin, o));
-  }
-  nmax = __builtin_amdgcn_readfirstlane(nmax);
-  nmin = __builtin_amdgcn_readfirstlane(nmin == ~0u ? 0u : nmin);
-  const u32 nsym = (nmax + 3 + 3) & ~3u;  // entries, in groups of 4: symbols, then 3 finish
-  const uint8_t* sp = syms + s0;
-  const u32 a = (u32)(((uintptr_t)out + o0) & (ENC_UNIT - 1));
-  u64 cap = o1 - o0;
-  if (cap > 0xFFFFFF00ull - a) cap = 0xFFFFFF00ull - a;
-  if (!coder) {
-    s_out[lane].gbase = out + o0 - a;
-    s_out[lane].lo_ok = a;
-    s_out[lane].hi_ok = a + (u32)cap;
-  }
-  __syncthreads();
-
-  if (coder) {
-    SplCoder<DIV, SM> e;
-    e.low = 0;
-    e.range = ~0ull;
-    e.err = 0;
-    // input: 16-B aligned loads of the lane's stream (clamped to its last block), shifted by the
-    // stream's offset o in two selects of dwords and one v_alignbyte_b32
-    const u32 o = (u32)((uintptr_t)sp & 15);
-    const bool has_in = live && n > 0;
-    const uint4* ab = has_in ? reinterpret_cast<const uint4*>(sp - o)
-                             : reinterpret_cast<const uint4*>(g_sink);
-    const u32 glast = has_in ? (u32)((o + n - 1) >> 4) : 0u;
-    const u32 m2 = (o & 8) ? ~0u : 0u, m1 = (o & 4) ? ~0u : 0u;
-    uint4 ax = ab[0];
-    uint4 ay = ab[min(1u, glast)];
-    u32 cons_seen = 0;
-    for (u32 i16 = 0; i16 < nsym; i16 += 16) {
-      const u32 b = i16 >> 4;
-      const u32 W[8] = {ax.x, ax.y, ax.z, ax.w, ay.x, ay.y, ay.z, ay.w};
-      ax = ay;
-      ay = ab[min(b + 2, glast)];  // one block ahead
-      u32 V[6], U[5], w4[4];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) V[i] = mselc(m2, W[i + 2], W[i]);
-#pragma unroll
-      for (int i = 0; i < 5; ++i) U[i] = mselc(m1, V[i + 1], V[i]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) w4[i] = __builtin_amdgcn_alignbyte(U[i + 1], U[i], o);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const u32 i0 = i16 + 4 * q;
-        if (i0 >= nsym) break;
-        // room for four entries
-        for (u32 spin = 0; i0 + 4 > cons_seen + SPL_F && spin < SPL_SPIN_MAX; ++spin) {
-          cons_seen = lds_acquire(&s_cons);
-          if (i0 + 4 > cons_seen + SPL_F) __builtin_amdgcn_s_sleep(1);
-        }
-        const u32 w = w4[q];
-        if (i0 + 4 <= nmin) {
-#pragma unroll
-          for (int j = 0; j < 4; j += 2) {
-            const u32 sl0 = (i0 + j) % SPL_F, sl1 = (i0 + j + 1) % SPL_F;
-            const uint2 t0 = s_tab[(w >> (8 * j)) & 255u], t1 = s_tab[(w >> (8 * j + 8)) & 255u];
-            u64 L0, L1;
-            u32 b0, b1;
-            const bool r0 = spl_step<DIV, SM>(e, m, t0, L0, b0);
-            const SplCoder<DIV, SM> ea = e;
-            bool r1 = spl_step<DIV, SM>(e, m, t1, L1, b1);
-            if (__builtin_expect(__any((int)(r0 | r1)), 0)) {
-              if (r0) {
-                e = ea;
-                b0 = spl_rare(e, b0);
-                r1 = spl_step<DIV, SM>(e, m, t1, L1, b1);
-              }
-              if (r1) b1 = spl_rare(e, b1);
-              if (b0 > 24) s_fifo_lo[sl0][lane] = (u32)L0;
-              if (b1 > 24) s_fifo_lo[sl1][lane] = (u32)L1;
-            }
-            s_fifo[sl0][lane] = make_uint2(hi32(L0), b0);
-            s_fifo[sl1][lane] = make_uint2(hi32(L1), b1);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const u32 i = i0 + j, sl = i % SPL_F;
-            uint2 en = make_uint2(0u, 0u);
-            if (i < n32) {
-              u64 L;
-              u32 bb;
-              if (spl_step<DIV, SM>(e, m, s_tab[(w >> (8 * j)) & 255u], L, bb)) {
-                bb = spl_rare(e, bb);
-                s_fifo_lo[sl][lane] = (u32)L;
-              }
-              en = make_uint2(hi32(L), bb);
-            } else if (i < n32 + 3) {  // Encoder::finish (encoder.rs:40-46): the 8 bytes of low
-              const u32 f = i - n32;
-              en = make_uint2(hi32(e.low << (24 * f)), f < 2 ? 24u : 16u);
-            }
-            s_fifo[sl][lane] = en;
-          }
-        }
-        lds_release(&s_prod, i0 + 4);
-      }
-    }
-    if (live) {
-      if (SM == 1) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
-      s_err[lane] = e.err;
-    }
-    __syncthreads();
-    return;
-  }
-
-  // ---- output wave ----
-  Enc e;
-#ifdef RC_FILL
-  e.fill = 0;
-#endif
-  e.low = 0;
-  e.range = 0;
-  e.acc = 0;
-  e.B = 8 * a;
-  e.fpos = 0;
-  e.err = 0;
-  e.ring = (u32)(uintptr_t)(__attribute__((address_space(3))) u32*)(s_ring + lane);
-  const u32* wring = s_ring;
-  const EncOut* wout = s_out;
-  u32 prod_seen = 0;
-  for (u32 i0 = 0; i0 < nsym; i0 += 4) {
-    for (u32 spin = 0; i0 + 4 > prod_seen && spin < SPL_SPIN_MAX; ++spin) {
-      prod_seen = lds_acquire(&s_prod);
-      if (i0 + 4 > prod_seen) __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u32 sl = (i0 + j) % SPL_F;
-      const uint2 en = s_fifo[sl][lane];
-      if (__builtin_expect(__any((int)(en.y > 24u)), 0)) {
-        if (en.y > 24u) {  // a rare symbol: its bytes one by one from the top of L, then zeros
-          u64 L = ((u64)en.x << 32) | s_fifo_lo[sl][lane];
-          for (u32 t = 0; t < en.y; t += 8) {
-            enc_emit_byte(e, (u32)(L >> 56));
-            L <<= 8;
-          }
-        } else {
-          spl_emit(e, en.x, en.y);
-        }
-        enc_flush(e, lane, wring, wout);
-      } else {
-        spl_emit(e, en.x, en.y);
-      }
-    }
-    lds_release(&s_cons, i0 + 4);
-    enc_flush(e, lane, wring, wout);
-  }
-  const u32 len = (e.B >> 3) - a;
-  u32 wend = enc_wpos(e);
-  if (e.B & 31) {
-    ring_put(e.ring, (e.B >> 5) & (ENC_RING - 1), (u32)(e.acc << (32 - (e.B & 31))));
-    wend += 4;
-  }
-  const u32 end = a + len;
-  if (end < s_out[lane].hi_ok) s_out[lane].hi_ok = end;
-  while (__any((int)(e.fpos < wend))) enc_round(e, e.fpos < wend, lane, wring, wout);
-  __syncthreads();  // the coder's flags
-  if (live) {
-    u32 err = s_err[lane];
-    if (!err && (u64)len > cap) err = RC_F_CAPACITY;
-    out_len[k] = too_long ? 0u : len;
-    flags[k] = too_long ? RC_F_TOO_LONG : err;
-  }
-}
-
-namespace {
-// Split encoder for a launch (RC_ENC_SPLIT=0 / 1 overrides; read at every launch, as tests
-// switch it): when the chunks give k_encode_static at most 2 waves per SIMD
-bool use_split(u32 n_chunks) {
-  const char* e = getenv("RC_ENC_SPLIT");
-  if (e && *e) return strtol(e, nullptr, 10) != 0;
-  static std::atomic<u32> cache[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return false;
-  u32 cus = dev < 64 ? cache[dev].load(std::memory_order_relaxed) : 0u;
-  if (!cus) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        v <= 0)
-      v = 256;
-    cus = (u32)v;
-    if (dev < 64) cache[dev].store(cus, std::memory_order_relaxed);
-  }
-  return (u64)n_chunks <= (u64)cus * 512;
-}
-}  // namespace
-#endif  // RC_ENC_SPLIT2
-
 hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a, int div, int smv,
                                    const uint8_t* syms, const u64* sym_off, u32 n_chunks,
                                    uint8_t* out, const u64* out_off, u64* out_len, u32* flags) {
-#ifdef RC_ENC_SPLIT2
-  const bool split = use_split(n_chunks);
-  const dim3 grid(split ? (n_chunks + 63) / 64 : (n_chunks + WG - 1) / WG), block(split ? 128 : WG);
-#define RC_ENC_LAUNCH(D, S)                                                                   \
-  do {                                                                                        \
-    if (split)                                                                                \
-      hipLaunchKernelGGL((k_encode_split<D, S>), grid, block, 0, stream, a, syms, sym_off,   \
-                         n_chunks, out, out_off, out_len, flags);                             \
-    else                                                                                      \
-      hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, stream, a, syms, sym_off,  \
-                         n_chunks, out, out_off, out_len, flags);                             \
-  } while (0)
-#else
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
 #define RC_ENC_LAUNCH(D, S)                                                                   \
   hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, stream, a, syms, sym_off,      \
                      n_chunks, out, out_off, out_len, flags)
-#endif
 #ifdef RC_DEV_ONLY  // scratch builds for kernel tuning: the headline variants only
   if (div != DIV_POW2 || smv == 0) return hipErrorInvalidValue;
   if (smv == 2) RC_ENC_LAUNCH(DIV_POW2, 2); else RC_ENC_LAUNCH(DIV_POW2, 1);
