@@ -357,9 +357,9 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
     }
   }
   // small bucket models (the decoder's LUT 4, rc_static.h): 8-B buckets {16 s0 | 16 s1 << 16,
-  // cum[s1]} (s1's absolute cum; 0 without a split, where s1 = s0), at most 2^SMB_LUT_BITS of
-  // them and at least 8 frequencies each, so the bucket's byte address is (q >> la_shift) &
-  // la_mask with la_shift = lut_shift - 3 >= 0
+  // 0x4B400000 + cum[s1]} (s1's absolute cum; 0 without a split, where s1 = s0), at most
+  // 2^SMB_LUT_BITS of them and at least 8 frequencies each, so the bucket's byte address is
+  // (q >> la_shift) & la_mask with la_shift = lut_shift - 3 >= 0
   if (!a.direct && total_freq <= 65536) {
     const u32 bits = std::min<u32>(SMB_LUT_BITS, bl - 3);  // (total > 2048: bl >= 12)
     u32 shift = 0;
@@ -370,7 +370,8 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
       const u32 e = lt[b], s0 = e & 255u, s1 = (e >> 8) & 255u, split = e >> 16;
       // (padded buckets repeat the last real one, (total - 1) >> shift)
       const u32 br = (u32)std::min<size_t>(b, (total_freq - 1) >> shift);
-      const u32 cum1 = split == 0xFFFFu ? 0u : (br << shift) + split;
+      // (as hint_floor's bits, 0x4B400000 + cum[s1]: the decoder compares the hint's raw bits)
+      const u32 cum1 = 0x4B400000u + (split == 0xFFFFu ? 0u : (br << shift) + split);
       l8[2 * b] = 16 * s0 | (16 * s1) << 16;
       l8[2 * b + 1] = cum1;
     }
