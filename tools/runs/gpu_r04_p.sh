@@ -1,0 +1,20 @@
+# Round 4, call P: the LUT 4 decoder in 640-lane workgroups (RC_DEC_SMB_WG=640: 5 waves per SIMD
+# instead of 4): the parity and ring suites on it, then Zipf decode against the 256-lane default
+# at 2^20, 2^19 and 2^18 chunks, 3 interleaved rounds, one box.
+set -e
+O=$GRAFT_REPO_ROOT/gpurun_out/r04p
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+RC_DEC_SMB_WG=640 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_ring.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+ONE="--no-cpu-baseline --no-zipf --no-adaptive --no-model-build --no-container --no-host-stream"
+run() {  # tag wg n
+  RC_DEC_SMB_WG=$2 timeout -k 10 300 python3 bench.py --config zipf --global-chunks $3 $ONE --steps 5 --warmup 1 > $O/$1.json 2> $O/$1.err || { tail -5 $O/$1.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['encode_gsym_s'], d['decode_gsym_s'], d['value'])" $O/$1.json "$1"
+}
+for r in 1 2 3; do
+  for n in 1048576 524288 262144; do
+    run wg256_${n}_$r 256 $n
+    run wg640_${n}_$r 640 $n
+  done
+done
