@@ -47,9 +47,6 @@
 #ifndef DEC_SPEC
 #define DEC_SPEC 1           // every SM decoder takes the speculative step (verify deferred)
 #endif
-#ifndef DEC_XSPEC
-#define DEC_XSPEC 0          // pair decoder: the next symbol's hint from data - (low + r cum)
-#endif
 #ifndef ENC_PAIR
 #define ENC_PAIR 1           // small-model encoders test the rare path once per two symbols
 #endif
@@ -99,10 +96,12 @@ struct ModelArgs {
 // holds the symbol table at address 0, one 16-B entry {cum, c, total/c as f32, s} per symbol at
 // byte 16 s, then up to 2^SMB_LUT_BITS 8-B buckets {16 s0 | 16 s1 << 16, 0x4B400000 + cum[s1]}
 // at SMB_LUT_OFF: the candidate's table address is one v_cndmask_b32 over its bucket entry's
-// halves, and the candidate's whole entry one ds_read_b128.  2^12 buckets (32 KiB) run in
-// 512-lane workgroups, so that the LDS per wave stays that of 2^11 buckets in 256-lane ones.
+// halves, and the candidate's whole entry one ds_read_b128.  2^12 buckets (32 KiB: buckets of
+// 16 frequencies at total 2^16, where the Zipf(1.2) model has no bucket with three symbol
+// starts) run in 512-lane workgroups, so that the LDS per wave stays that of 2^11 buckets in
+// 256-lane ones (4 waves per SIMD); models with total <= 2^14 get fewer buckets and 256 lanes.
 #ifndef SMB_LUT_BITS
-#define SMB_LUT_BITS 11u
+#define SMB_LUT_BITS 12u
 #endif
 #define SMB_WG(lut_entries) ((lut_entries) > 2048u ? 512u : (u32)WG)
 #define SMB_TAB_WORDS 1024u                      // the symbol table
