@@ -159,6 +159,58 @@ def test_wide_direct_lut_models(ctx, total):
             assert (dec[k] == d).all(), k
 
 
+@pytest.mark.parametrize("total", [2049, 4096, 10000, 16384, 16385, 32769, 65535, 65536])
+@pytest.mark.parametrize("shape", ["zipf", "runs"])
+def test_small_bucket_models(ctx, total, shape):
+    """2048 < total <= 2^16 decodes through the small bucket-model decoder (LUT 4): up to 2^11
+    buckets in 256-lane workgroups for total <= 2^14, 2^12 buckets in 512-lane ones above
+    (rc_static.h SMB_WG), across the boundary and with pow2 and magic-division totals.  "zipf":
+    a Zipf(1.2) table; "runs": runs of c = 1 and c = 2 symbols between large ones, so buckets
+    hold three or more symbol starts and the candidate pair misses (the exact fix-up).  Encode
+    bytes and decoded symbols against the oracle; garbage streams decode like find_index."""
+    rng = np.random.default_rng(total * 7 + (shape == "runs"))
+    n = 256
+    if shape == "zipf":
+        w = 1.0 / np.arange(1, n + 1) ** 1.2
+        c = np.maximum(1, np.floor(w / w.sum() * total)).astype(np.int64)
+    else:
+        c = rng.choice([1, 1, 2, 3], n).astype(np.int64)
+        c[::37] = total // 16
+    c[int(np.argmax(c))] += total - c.sum()
+    assert c.min() >= 1 and c.sum() == total
+    c = c.astype(np.uint32)
+    cum = cum_of(c)
+    m = rc.StaticModel(c, cum, total)
+    p = c / c.sum()
+    lens = list(rng.choice([0, 1, 15, 16, 63, 64, 65, 1000, 4099], 48))
+    chunks = [rng.choice(n, L, p=p).astype(np.uint8) for L in lens]
+    # runs: also sequences of the rarest symbols, which keep range small and the fix-ups busy
+    if shape == "runs":
+        rare = np.nonzero(c <= 2)[0]
+        chunks += [rng.choice(rare, 2000).astype(np.uint8) for _ in range(8)]
+        lens += [2000] * 8
+    caps = [rc.slot_capacity(L, m.max_bits_per_symbol() + 1) for L in lens]
+    out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=True, seed=total)
+    codes = []
+    for k, ch in enumerate(chunks):
+        f, b, L = cpu.encode(c, cum, total, ch)
+        assert (fl[k], ol[k]) == (f, L), k
+        assert bytes(out[out_off[k]: out_off[k] + ol[k]]) == b, k
+        codes.append(b)
+    dec, fd = run_decode(m, codes, lens, misalign=True, seed=total + 1)
+    for k, ch in enumerate(chunks):
+        assert fd[k] == 0 and (dec[k] == ch).all(), k
+    garbage = [rng.integers(0, 256, int(rng.integers(8, 400))).astype(np.uint8).tobytes()
+               for _ in range(64)]
+    counts = [int(rng.integers(0, 300)) for _ in garbage]
+    dec, fd = run_decode(m, garbage, counts, misalign=False, seed=total + 2)
+    for k in range(len(garbage)):
+        f, d = cpu.decode(c, cum, total, garbage[k], counts[k])
+        assert fd[k] == f, k
+        if f == 0:
+            assert (dec[k] == d).all(), k
+
+
 @pytest.mark.parametrize("total,c_big", [(65536, 65536 - 255), (32768, 32768 - 255),
                                          (4096, 4096 - 255), (65536, 1 << 15)])
 @pytest.mark.parametrize("misalign", [False, True])
