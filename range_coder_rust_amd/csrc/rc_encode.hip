@@ -141,8 +141,13 @@ static __device__ __forceinline__ void enc_rare(Enc& e) {
 // compiler's form is a shift, an and and an add)
 static __device__ __forceinline__ void enc_out(Enc& e, u32 lh, u32 nb) {
 #ifndef RC_EXP_NOOUT  // (scratch builds: the coder's arithmetic alone, output dropped; timing only)
-  const u32 bytes = __builtin_amdgcn_ubfe(lh, 32u - nb, nb);  // the top nb bits (0 if nb == 0)
-  e.acc = (e.acc << nb) | bytes;
+  // acc = acc << nb | the top nb bits of lh (nb = 8n, n <= 3), as two byte permutations that
+  // share one selector: hi32({a1:a0} << nb) and hi32({a0:lh} << nb), selector byte j = 4 + j - n
+  // (for nb = 0 both are the identity).  (From C: a subtract, a bit-field extract, a 64-bit shift
+  // and an OR.)
+  const u32 sel = hi32(0x0706050403020100ull << nb);
+  const u32 a0 = (u32)e.acc, a1 = hi32(e.acc);
+  e.acc = ((u64)__builtin_amdgcn_perm(a1, a0, sel) << 32) | __builtin_amdgcn_perm(a0, lh, sel);
   u32 soff, saddr;
   asm("v_and_b32 %0, %1, %2" : "=v"(soff) : "i"((ENC_RING - 1) << 5), "v"(e.B));
   asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(saddr) : "v"(soff), "v"(e.ring));
