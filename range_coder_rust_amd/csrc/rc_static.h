@@ -92,7 +92,8 @@ struct ModelArgs {
   u32 la_mask;
 };
 
-// Small bucket models (k_decode_static LUT 4: 2048 < total <= 2^16, not pair-decoded).  LDS
+// Small bucket models (k_decode_static LUT 4: 2048 < total <= 2^16; the pair decoder, LUT 3, is
+// opt-in, RC_DEC_PAIR).  LDS
 // holds the symbol table at address 0, one 16-B entry {cum, c, total/c as f32, s} per symbol at
 // byte 16 s, then up to 2^SMB_LUT_BITS 8-B buckets {16 s0 | 16 s1 << 16, 0x4B400000 + cum[s1]}
 // at SMB_LUT_OFF: the candidate's table address is one v_cndmask_b32 over its bucket entry's
