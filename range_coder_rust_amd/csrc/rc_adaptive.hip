@@ -199,6 +199,22 @@ struct AOut {  // per-lane output geometry
   u32 end;     // a + capacity (clamped to 32 bits): origin-relative end of the slot
 };
 
+// the same for nb = 8n <= 24 (the coder's settled bytes): every word is hi32({Wi:Wi+1} << nb),
+// byte j from byte 4 + j - n of the pair, so four v_perm_b32 share one selector,
+// hi32(0x0706050403020100 << nb).  (From C: four 64-bit shifts and the register-pair copies that
+// assemble their operands.)
+static __device__ __forceinline__ void out_push8(AEnc& e, u32 hl, u32 nb) {
+  const u32 sel = hi32(0x0706050403020100ull << nb);
+  const u32 w0 = __builtin_amdgcn_perm(e.W0, e.W1, sel);
+  const u32 w1 = __builtin_amdgcn_perm(e.W1, e.W2, sel);
+  const u32 w2 = __builtin_amdgcn_perm(e.W2, e.W3, sel);
+  e.W3 = __builtin_amdgcn_perm(e.W3, hl, sel);
+  e.W0 = w0;
+  e.W1 = w1;
+  e.W2 = w2;
+  e.B += nb;
+}
+
 // shift the register left by nb bits (0..32) and append the top nb bits of hl
 static __device__ __forceinline__ void out_push(AEnc& e, u32 hl, u32 nb) {
   e.W0 = hi32((((u64)e.W0 << 32) | e.W1) << nb);
@@ -245,7 +261,7 @@ static __device__ __forceinline__ bool enc_code(AEnc& e, u32 cum, u32 c, u32 tot
   e.range = mul_r(r, c);
   e.low += mul_r(r, cum);
   const u32 nb = clz32(hi32(e.low) ^ hi32(e.low + e.range)) & 24u;
-  out_push(e, hi32(e.low), nb);
+  out_push8(e, hi32(e.low), nb);
   e.low <<= nb;
   e.range <<= nb;
   return hi32(e.range) < 0x10000u;
@@ -256,7 +272,7 @@ static __device__ __forceinline__ void enc_reduce(AEnc& e, const AOut& g, bool w
   while (e.range < TOP16) {
     e.range = ~e.low & (TOP16 - 1);
     if (e.B > 112) out_flush(e, g, wr);
-    out_push(e, hi32(e.low), 8);
+    out_push8(e, hi32(e.low), 8);
     e.low <<= 8;
     e.range <<= 8;
   }
