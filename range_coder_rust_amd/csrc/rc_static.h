@@ -47,9 +47,6 @@
 #ifndef DEC_SPEC
 #define DEC_SPEC 1           // every SM decoder takes the speculative step (verify deferred)
 #endif
-#ifndef DEC_XSPEC
-#define DEC_XSPEC 0          // pair decoder: table entry and ring pair read one symbol ahead
-#endif
 #ifndef ENC_PAIR
 #define ENC_PAIR 1           // small-model encoders test the rare path once per two symbols
 #endif
