@@ -23,6 +23,7 @@
 // no-carry bytes + up to 7 range_reduction_expansion bytes each); unpaired (and wide) models
 // at most 7 symbols of <= 3 bytes and one rare symbol (<= 8 no-carry + 7 reduction bytes).
 static_assert(FLUSH_AT % 4 == 0, "FLUSH_AT counts whole dwords");
+static_assert(ENC_UNIT == 64 && ENC_RING % 4 == 0, "a flush granule's 4 ring dwords must not wrap");
 static_assert(FLUSH_AT - 1 + 6 * 3 + 2 * (3 + 7) <= 4 * ENC_RING - 1,
               "paired small-model encoder may overrun its output ring");
 static_assert(FLUSH_AT - 1 + 7 * 3 + (8 + 7) <= 4 * ENC_RING - 1,
@@ -70,12 +71,12 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
     const bool hc = __shfl((int)has, c) != 0;
     const u32 fp = (u32)__shfl((int)e.fpos, c);
     if (hc) {
-      const u32 slot = (fp >> 2) + 4 * g;
-      const u32* rp = wring + c;
-      const uint4 v = make_uint4(__builtin_bswap32(rp[((slot + 0) & (ENC_RING - 1)) * 64]),
-                                 __builtin_bswap32(rp[((slot + 1) & (ENC_RING - 1)) * 64]),
-                                 __builtin_bswap32(rp[((slot + 2) & (ENC_RING - 1)) * 64]),
-                                 __builtin_bswap32(rp[((slot + 3) & (ENC_RING - 1)) * 64]));
+      // fp is a multiple of ENC_UNIT = 64 B, so the granule's first slot is a multiple of 4 and
+      // its 4 dwords never wrap the ring: one address, two ds_read2st64_b32
+      const u32 slot = ((fp >> 2) + 4 * g) & (ENC_RING - 1);
+      const u32* rp = wring + c + slot * 64;
+      const uint4 v = make_uint4(__builtin_bswap32(rp[0]), __builtin_bswap32(rp[64]),
+                                 __builtin_bswap32(rp[128]), __builtin_bswap32(rp[192]));
       const EncOut o = wout[c];
       const u32 p0 = fp + 16 * g;
       if (p0 >= o.lo_ok && p0 + 16 <= o.hi_ok) {
@@ -409,6 +410,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
     c2 = tp[2];
     c3 = tp[3];
   }
+#pragma unroll 1  // (64 symbols per trip already; a second copy only grows the code)
   for (u64 t = 0; t < tmin; ++t) {
     uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
     if (t + 1 < tmin) {
