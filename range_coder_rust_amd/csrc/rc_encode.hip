@@ -410,7 +410,6 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
     c2 = tp[2];
     c3 = tp[3];
   }
-#pragma unroll 1  // (64 symbols per trip already; a second copy only grows the code)
   for (u64 t = 0; t < tmin; ++t) {
     uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
     if (t + 1 < tmin) {
