@@ -54,6 +54,12 @@ static __device__ __forceinline__ void ring_put(u32 col, u32 slot, u32 v) {
 // byte position of the incomplete dword (everything below it has been pushed to the ring)
 static __device__ __forceinline__ u32 enc_wpos(const Enc& e) { return (e.B >> 5) << 2; }
 
+// enc_wpos(e) - fpos >= T for T a multiple of 4, tested as (B >> 3) - fpos >= T: fpos + T is a
+// multiple of 4, so rounding B >> 3 down to one (enc_wpos) cannot cross it (one shift fewer)
+static __device__ __forceinline__ bool enc_ready(const Enc& e, u32 T) {
+  return (e.B >> 3) - e.fpos >= T;
+}
+
 // Per-chunk output geometry shared with the other lanes of the wave (flush rounds)
 struct EncOut {
   uint8_t* gbase;  // 64-B aligned base of the slot
@@ -104,10 +110,10 @@ static __device__ __forceinline__ void enc_flush(Enc& e, u32 lane, const u32* wr
                                                  const EncOut* wout) {
   // (the first test stays inline in every caller: written as a plain while loop, the compiler
   // shared one test block among the call sites and copied the coder state at each jump to it)
-  if (__builtin_expect(__any((int)(enc_wpos(e) - e.fpos >= FLUSH_AT)), 0)) {
+  if (__builtin_expect(__any((int)enc_ready(e, FLUSH_AT)), 0)) {
     do {
-      enc_round(e, enc_wpos(e) - e.fpos >= ENC_UNIT, lane, wring, wout);
-    } while (__any((int)(enc_wpos(e) - e.fpos >= FLUSH_AT)));
+      enc_round(e, enc_ready(e, ENC_UNIT), lane, wring, wout);
+    } while (__any((int)enc_ready(e, FLUSH_AT)));
   }
 }
 
