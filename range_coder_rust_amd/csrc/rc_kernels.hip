@@ -379,6 +379,7 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
     a.lut_shift = shift;
     a.la_shift = shift - 3;
     a.la_mask = ((u32)lt.size() - 1) << 3;
+    a.la_magic = ldexpf(1.5f, 23 + (int)a.la_shift);
     a.lut_max = (u32)lt.size() - 1;
     lut.swap(l8);
   }

@@ -90,6 +90,7 @@ struct ModelArgs {
                      // entry per bucket {cum0 | c0 << 16, cum1 | c1 << 16, total/c0, total/c1}
   u32 la_shift;      // small bucket models (LUT 4): bucket byte address = (q >> la_shift) & la_mask
   u32 la_mask;
+  float la_magic;    // 1.5 * 2^(23 + la_shift): fma(X, G, la_magic)'s low bits are q >> la_shift
 };
 
 // Small bucket models (k_decode_static LUT 4: 2048 < total <= 2^16; the pair decoder, LUT 3, is
