@@ -192,7 +192,7 @@ static __device__ __forceinline__ bool enc_core(Enc& e, const ModelArgs& m, uint
     c = bad ? 1u : t.y;
     cum = bad ? 0u : t.x;
   }
-  const u64 r = range_par_total<DIV>(e.range, m);
+  const u64 r = range_par_total<DIV, SM>(e.range, m);
   if (SM) {  // r < 2^56, c, cum <= 2^16: low half by v_mad_u64_u32, high by v_mad_u32_u24
     const u32 rl = (u32)r, rh = hi32(r);
     const u64 R0 = (u64)rl * c;                   // range_coder.rs:65

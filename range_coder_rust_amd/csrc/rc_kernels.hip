@@ -52,6 +52,7 @@ __global__ __launch_bounds__(WG) void k_synth_generic(u64 seed, const uint8_t* _
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 struct rc_ctx {
@@ -264,6 +265,8 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
   const bool pow2 = (total_freq & (total_freq - 1)) == 0;
   a.lg = pow2 ? (u32)__builtin_ctz(total_freq) : 0u;
   a.magic = ~0ull / (u64)total_freq;
+  a.inv_up = 1.0 / (double)total_freq;  // rounded up: inv_up * total >= 1 exactly
+  if (std::fma(a.inv_up, (double)total_freq, -1.0) < 0.0) a.inv_up = std::nextafter(a.inv_up, 2.0);
   // bucket table of 2^bits buckets: s0 = symbol containing the bucket's first frequency, s1 =
   // the next symbol with c > 0 starting inside the bucket, split = its offset (0xFFFF: none);
   // padded to a power of two (the kernel masks the bucket index) with the last bucket, so

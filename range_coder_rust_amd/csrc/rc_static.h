@@ -91,6 +91,7 @@ struct ModelArgs {
   u32 la_shift;      // small bucket models (LUT 4): bucket byte address = (q >> la_shift) & la_mask
   u32 la_mask;
   float la_magic;    // 1.5 * 2^(23 + la_shift): fma(X, G, la_magic)'s low bits are q >> la_shift
+  double inv_up;     // 1 / total rounded up (small models, DIV_MAGIC: range / total in f64)
 };
 
 // Small bucket models (k_decode_static LUT 4: 2048 < total <= 2^16; the pair decoder, LUT 3, is
@@ -120,9 +121,27 @@ struct ModelArgs {
 
 
 // RangeCoder::range_par_total (range_coder.rs:38-40): range / total, exact.
-template <int DIV>
+// SM (256 <= total <= 2^16), total not a power of two: two f64 steps with u = 1/total rounded
+// up.  q1 = trunc(rh u) = floor(rh / total): the exact product is >= rh / total, and exceeds it
+// by at most rh 2^-52 / total < 2^-28 while the distance to the next integer is >= 1 / total >=
+// 2^-16, so neither the error nor the product's rounding (to nearest, or toward zero; q1 < 2^24
+// is representable) reaches another integer.  Then n = (rh - q1 total) 2^32 + rl < total 2^32 <=
+// 2^48 is exact in f64 (one fma), and q0 = trunc(n u) = floor(n / total) by the same argument
+// (error < 2^-4 / total, rounding ulp 2^-20 below 2^32).  range / total = q1 2^32 + q0.  Ten
+// instructions instead of the 64 x 64 high product, its fix-up and their register copies.
+#ifndef RC_DIV_F64
+#define RC_DIV_F64 1  // 0: the 64 x 64 high product for small models too (scratch A/B builds)
+#endif
+template <int DIV, int SM = 0>
 static __device__ __forceinline__ u64 range_par_total(u64 range, const ModelArgs& m) {
   if (DIV == DIV_POW2) return range >> m.lg;
+  if (SM && RC_DIV_F64) {
+    const u32 rh = hi32(range), rl = (u32)range;
+    const u32 q1 = (u32)((double)rh * m.inv_up);
+    const u32 rem = rh - __umul24(q1, m.total);
+    const u32 q0 = (u32)(__builtin_fma((double)rem, 4294967296.0, (double)rl) * m.inv_up);
+    return ((u64)q1 << 32) | q0;
+  }
   u64 q = __umul64hi(range, m.magic);  // q in {floor - 1, floor}
   u64 rem = range - q * (u64)m.total;
   return rem >= (u64)m.total ? q + 1 : q;
