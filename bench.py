@@ -135,6 +135,16 @@ def equal_chunked(torch, a, b, step=1 << 30):
     return True
 
 
+def lib_sha256(path):
+    """sha256 of a built library (keys profiles/traffic.json entries to the build they measured)"""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
 def run_leg(torch, dist, leg, steps, warmup, world):
     """W untimed steps, then exactly K timed steps bracketed by barrier + synchronize."""
     for _ in range(warmup):
@@ -427,18 +437,27 @@ def main():
                        gbps=alg_bytes / res["dec_ms"] / 1e6),
     }
     dom = "decode" if res["dec_ms"] >= res["enc_ms"] else "encode"
-    traffic = None
+    # roofline.traffic: PMC-measured HBM bytes of this exact library build only (the entry is
+    # keyed to the sha256 of the librc_amd.so it was profiled on; tools/pmc_traffic.py)
+    traffic, traffic_note = None, "no profile of this workload in " + os.path.relpath(args.traffic, ROOT)
     try:
         with open(args.traffic) as f:
             tr = json.load(f)
         key = f"{args.config}:{n}:{L}:{dom}"
         if key in tr:
-            traffic = tr[key]["hbm_bytes_per_launch"]
+            from range_coder_rust_amd import _native
+            if tr[key].get("lib_sha256") == lib_sha256(_native.LIB_PATH):
+                traffic = tr[key]["hbm_bytes_per_launch"]
+                traffic_note = f"PMC, this build ({tr[key].get('round')})"
+            else:
+                traffic_note = (f"stale: {tr[key].get('round')} profiled another build of "
+                                f"librc_amd.so; not reported")
     except (OSError, ValueError, KeyError):
         traffic = None
     achieved = kern[dom]["gbps"]
     roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBPS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic, kernel=dom,
+                    frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic,
+                    traffic_source=traffic_note, kernel=dom,
                     alg_bytes_per_launch=alg_bytes)
 
     extras = {}

@@ -37,7 +37,27 @@ typedef u32 u32x3 __attribute__((ext_vector_type(3)));
 #ifndef RC_FILL_OP
 #define RC_FILL_OP 0
 #endif
-// the filler register: a VGPR pair for the 64-bit instructions, one VGPR otherwise
+// the filler register: a VGPR pair for the 64-bit instructions, one VGPR otherwise; the scalar
+// and branch fillers (RC_FILL_OP >= 20) carry an SGPR, the LDS filler a VGPR address
+#if RC_FILL_OP >= 20
+struct rc_fill_t {
+  u32 x;
+  __device__ rc_fill_t& operator=(int v) { x = (u32)v; return *this; }
+};
+static __device__ __forceinline__ void rc_filler_one(rc_fill_t& f) {
+  switch (RC_FILL_OP) {
+    // (a fixed SGPR, clobbered: a state member would turn divergent at the decoders' redo
+    // paths and could not stay scalar)
+    case 20: asm volatile("s_add_u32 s100, s100, 1" ::: "s100", "scc"); break;              // SALU
+    case 21: asm volatile("s_cmp_eq_u32 s100, 1\n\ts_cbranch_scc1 0" ::: "s100", "scc"); break;  // SALU + branch
+    case 22: asm volatile("s_cmp_eq_u32 s100, 1" ::: "s100", "scc"); break;                 // the SALU of 21
+    default: {  // 23: one LDS read of a table word, waited for by its consumer (a VALU add)
+      const u32 w = *(const volatile __attribute__((address_space(3))) u32*)(uintptr_t)(f.x & 0xFCu);
+      f.x += w;
+    }
+  }
+}
+#else
 #if RC_FILL_OP == 2 || RC_FILL_OP == 3 || RC_FILL_OP == 5 || RC_FILL_OP == 8 || RC_FILL_OP == 16
 typedef u64 rc_fill_t;
 #else
@@ -71,6 +91,7 @@ static __device__ __forceinline__ void rc_filler_one(u32& x) {
     default: asm volatile("v_xor_b32 %0, 1, %0" : "+v"(x)); break;
   }
 }
+#endif
 #define RC_FILLER(x)                                                   \
   do {                                                                 \
     _Pragma("unroll") for (int i_ = 0; i_ < RC_FILL; ++i_)             \
@@ -79,6 +100,61 @@ static __device__ __forceinline__ void rc_filler_one(u32& x) {
 #else
 #define RC_FILLER(x) \
   do {               \
+  } while (0)
+#endif
+
+// Scratch builds only (-DRC_STAMP, tools/stamp_probe.py): per-wave stamps.  Lane 0
+// of every wave records the constant 100 MHz clock (s_memrealtime) and the shader clock
+// (s_memtime) at kernel entry and exit, with HW_ID and XCC_ID, into a buffer of its translation
+// unit; rc_stamp_read_<tu>() copies the records out and clears them.  Vector stores only.
+struct RcStamp {
+  u64 rt0, rt1;  // s_memrealtime at entry / exit (100 MHz, one clock for the whole device)
+  u64 c0, c1;    // s_memtime at entry / exit (shader cycles)
+  u32 hwid, xcc; // HW_REG_HW_ID, HW_REG_XCC_ID
+  u32 nsym, pad; // symbols of lane 0's chunk
+};
+#define RC_STAMP_SLOTS 65536u
+#ifdef RC_STAMP
+#define RC_STAMP_DEFINE(tu)                                                                  \
+  static __device__ RcStamp g_stamp_##tu[RC_STAMP_SLOTS];                                    \
+  extern "C" int rc_stamp_read_##tu(void* dst, size_t n) {                                   \
+    if (n > RC_STAMP_SLOTS) n = RC_STAMP_SLOTS;                                              \
+    if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamp_##tu), n * sizeof(RcStamp)) != hipSuccess) \
+      return -1;                                                                             \
+    static RcStamp zero[1024];                                                               \
+    for (size_t i = 0; i < RC_STAMP_SLOTS; i += 1024)                                        \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_##tu), zero, sizeof(zero), i * sizeof(RcStamp)) \
+          != hipSuccess)                                                                     \
+        return -1;                                                                           \
+    return (int)n;                                                                           \
+  }
+#define RC_STAMP_BEGIN()                                  \
+  const u64 st_rt0_ = __builtin_amdgcn_s_memrealtime(); \
+  const u64 st_c0_ = __builtin_amdgcn_s_memtime()
+#define RC_STAMP_END(tu, slot, lane, nsym_) RC_STAMP_END_(tu, slot, lane, nsym_)
+#define RC_STAMP_END_(tu, slot, lane, nsym_)                                         \
+  do {                                                                               \
+    const u64 st_c1_ = __builtin_amdgcn_s_memtime();                                 \
+    const u64 st_rt1_ = __builtin_amdgcn_s_memrealtime();                            \
+    if ((lane) == 0 && (slot) < RC_STAMP_SLOTS) {                                    \
+      RcStamp* p_ = &g_stamp_##tu[slot];                                             \
+      p_->rt0 = st_rt0_;                                                             \
+      p_->rt1 = st_rt1_;                                                             \
+      p_->c0 = st_c0_;                                                               \
+      p_->c1 = st_c1_;                                                               \
+      p_->hwid = __builtin_amdgcn_s_getreg(0xF804); /* HW_ID, 32 bits */              \
+      p_->xcc = __builtin_amdgcn_s_getreg(0xF814);  /* XCC_ID */                      \
+      p_->nsym = (u32)(nsym_);                                                       \
+      p_->pad = 1u;                                                                  \
+    }                                                                                \
+  } while (0)
+#else
+#define RC_STAMP_DEFINE(tu)
+#define RC_STAMP_BEGIN() \
+  do {                   \
+  } while (0)
+#define RC_STAMP_END(tu, slot, lane, nsym) \
+  do {                                     \
   } while (0)
 #endif
 

@@ -28,8 +28,26 @@ static_assert(FLUSH_AT - 1 + 6 * 3 + 2 * (3 + 7) <= 4 * ENC_RING - 1,
               "paired small-model encoder may overrun its output ring");
 static_assert(FLUSH_AT - 1 + 7 * 3 + (8 + 7) <= 4 * ENC_RING - 1,
               "unpaired encoder may overrun its output ring");
+// Ring layout.  ENC_ROWS 1: a wave's 8 KiB ring holds 8 lane groups of 1 KiB (lanes 8g .. 8g+7);
+// in a group, slot j is the 32-B row j and lane L's dword sits at byte 4 (L & 7) of it.  A lane's
+// column base K then has no bits inside the row field (byte bits 5-9), so the slot of the dword
+// at stream bit B is at K | (B & 0x3E0): one v_and_or_b32 (the column-major layout below needs an
+// and plus a v_lshl_add_u32).  Four slots of a flush granule are four consecutive rows: two
+// ds_read2_b32 from one address.  Per-symbol pushes of the lanes of a 32-lane store group meet
+// in 4 banks per (L & 7) class, a conflict only when three or four of those lanes sit at the same
+// slot mod 4.
+// ENC_ROWS 0 (round 4): column-major, slot j of lane L at dword 64 j + L (stride 256 B).
+#ifndef ENC_ROWS
+#define ENC_ROWS 0  // (1 once measured on the GPU: variants/librc_amd_encrows.so)
+#endif
+#define ENC_SLOT_BYTES (ENC_ROWS ? 32u : 256u)  // byte distance between a lane's slots j, j + 1
+// LDS dword index of lane L's column inside its wave's ring
+static __device__ __forceinline__ u32 ring_col(u32 L) {
+  return ENC_ROWS ? (L >> 3) * 256u + (L & 7u) : L;
+}
 #define SINK_SLOTS 65536
 __device__ uint4 g_sink[SINK_SLOTS];  // dummy symbol tiles of dead lanes (contents irrelevant)
+RC_STAMP_DEFINE(enc)  // (scratch -DRC_STAMP builds only)
 
 struct Enc {
   u64 low, range;  // RangeCoder state (range_coder.rs:7-12)
@@ -41,14 +59,14 @@ struct Enc {
   rc_fill_t fill;  // scratch builds: the filler instructions' register
 #endif
   u32 err;         // first RC_F_* error of this chunk (SM: OR of staged table flags)
-  u32 ring;        // LDS byte address of this lane's ring column: dword j at ring + 256 * j.
+  u32 ring;        // LDS byte address of this lane's ring column: dword j at ring + j * ENC_SLOT_BYTES.
                    // The ring holds stream dwords as values (first byte in the top bits);
                    // the flush rounds byte-swap them on the way out.
 };
 
 // ring dword `slot` of the lane whose column is at LDS byte address `col`
 static __device__ __forceinline__ void ring_put(u32 col, u32 slot, u32 v) {
-  *(__attribute__((address_space(3))) u32*)(uintptr_t)(col + (slot << 8)) = v;
+  *(__attribute__((address_space(3))) u32*)(uintptr_t)(col + slot * ENC_SLOT_BYTES) = v;
 }
 
 // byte position of the incomplete dword (everything below it has been pushed to the ring)
@@ -78,11 +96,12 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
     const u32 fp = (u32)__shfl((int)e.fpos, c);
     if (hc) {
       // fp is a multiple of ENC_UNIT = 64 B, so the granule's first slot is a multiple of 4 and
-      // its 4 dwords never wrap the ring: one address, two ds_read2st64_b32
+      // its 4 dwords never wrap the ring: one address, two ds_read2 (st64 for column-major)
       const u32 slot = ((fp >> 2) + 4 * g) & (ENC_RING - 1);
-      const u32* rp = wring + c + slot * 64;
-      const uint4 v = make_uint4(__builtin_bswap32(rp[0]), __builtin_bswap32(rp[64]),
-                                 __builtin_bswap32(rp[128]), __builtin_bswap32(rp[192]));
+      constexpr u32 SD = ENC_SLOT_BYTES / 4;  // dwords between slots
+      const u32* rp = wring + ring_col(c) + slot * SD;
+      const uint4 v = make_uint4(__builtin_bswap32(rp[0]), __builtin_bswap32(rp[SD]),
+                                 __builtin_bswap32(rp[2 * SD]), __builtin_bswap32(rp[3 * SD]));
       const EncOut o = wout[c];
       const u32 p0 = fp + 16 * g;
       if (p0 >= o.lo_ok && p0 + 16 <= o.hi_ok) {
@@ -144,8 +163,9 @@ static __device__ __forceinline__ void enc_rare(Enc& e) {
 // before the shift), into the accumulator and pushed to the ring: the slot of the dword that
 // was incomplete before the symbol gets the 32 bits above the (new) incomplete ones; if it is
 // still incomplete the slot is rewritten later.  Slot (B >> 5) & (ENC_RING - 1) sits at byte
-// 256 slot of the column: (B & 0x3E0) << 3, an and plus one v_lshl_add_u32 (written out: the
-// compiler's form is a shift, an and and an add)
+// 32 slot of the column (ENC_ROWS): ring | (B & 0x3E0), one v_and_or_b32; column-major at byte
+// 256 slot, (B & 0x3E0) << 3, an and plus one v_lshl_add_u32 (written out: the compiler's form
+// is a shift, an and and an add)
 static __device__ __forceinline__ void enc_out(Enc& e, u32 lh, u32 nb) {
 #ifndef RC_EXP_NOOUT  // (scratch builds: the coder's arithmetic alone, output dropped; timing only)
   // acc = acc << nb | the top nb bits of lh (nb = 8n, n <= 3), as two byte permutations that
@@ -155,9 +175,14 @@ static __device__ __forceinline__ void enc_out(Enc& e, u32 lh, u32 nb) {
   const u32 sel = hi32(0x0706050403020100ull << nb);
   const u32 a0 = (u32)e.acc, a1 = hi32(e.acc);
   e.acc = ((u64)__builtin_amdgcn_perm(a1, a0, sel) << 32) | __builtin_amdgcn_perm(a0, lh, sel);
-  u32 soff, saddr;
-  asm("v_and_b32 %0, %1, %2" : "=v"(soff) : "i"((ENC_RING - 1) << 5), "v"(e.B));
-  asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(saddr) : "v"(soff), "v"(e.ring));
+  u32 saddr;
+  if (ENC_ROWS) {
+    saddr = (e.B & ((ENC_RING - 1) << 5)) | e.ring;
+  } else {
+    u32 soff;
+    asm("v_and_b32 %0, %1, %2" : "=v"(soff) : "i"((ENC_RING - 1) << 5), "v"(e.B));
+    asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(saddr) : "v"(soff), "v"(e.ring));
+  }
   e.B += nb;
   *(__attribute__((address_space(3))) u32*)(uintptr_t)saddr = (u32)(e.acc >> (e.B & 31u));
 #endif
@@ -332,8 +357,10 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
                                                         const u64* __restrict__ out_off,
                                                         u64* __restrict__ out_len,
                                                         u32* __restrict__ flags) {
+  RC_STAMP_BEGIN();
   __shared__ uint2 s_tab[256];
-  __shared__ u32 s_ring[WAVES * ENC_RING * 64];
+  // (1-KiB aligned: a column base has no bits in the row field, ENC_ROWS)
+  __shared__ __attribute__((aligned(1024))) u32 s_ring[WAVES * ENC_RING * 64];
   __shared__ EncOut s_out[WG];
   const u32 tid = threadIdx.x;
   {
@@ -383,7 +410,8 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   e.B = 8 * a;  // pad bytes in front of the slot (never stored)
   e.fpos = 0;
   e.err = 0;
-  e.ring = (u32)(uintptr_t)(__attribute__((address_space(3))) u32*)(s_ring + wave * ENC_RING * 64 + lane);
+  e.ring = (u32)(uintptr_t)(__attribute__((address_space(3))) u32*)(s_ring + wave * ENC_RING * 64 +
+                                                                     ring_col(lane));
 
   const uint8_t* sp = syms + s0;
   u64 head = (64 - ((uintptr_t)sp & 63)) & 63;  // symbols before the first 64-B aligned tile
@@ -464,6 +492,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   const u32 end = a + len;
   if (end < s_out[tid].hi_ok) s_out[tid].hi_ok = end;
   while (__any((int)(e.fpos < wend))) enc_round(e, e.fpos < wend, lane, wring, wout);
+  RC_STAMP_END(enc, blockIdx.x * WAVES + wave, lane, n);
   if (live) {
     if (SM == 1) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
     if (!e.err && (u64)len > cap) e.err = RC_F_CAPACITY;

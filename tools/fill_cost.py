@@ -21,7 +21,10 @@ sys.path.insert(0, ROOT)
 OPS = {0: "v_add_u32", 1: "v_lshrrev_b32", 2: "v_lshlrev_b64", 3: "v_mad_u64_u32",
        4: "v_mad_u32_u24", 5: "v_cmp_gt_u64_e64", 6: "v_alignbit_b32", 7: "v_perm_b32",
        8: "v_lshl_add_u64", 9: "v_cvt_f32_u32", 11: "v_lshl_add_u32", 12: "v_ffbh_u32",
-       13: "v_lshlrev_b32", 16: "v_lshrrev_b64"}
+       13: "v_lshlrev_b32", 16: "v_lshrrev_b64",
+       # round 5: the non-VALU classes (rc_common.h): scalar ALU, a compare + conditional branch,
+       # the compare alone, and one LDS read whose result a VALU add waits for
+       20: "s_add_u32", 21: "s_cmp+s_cbranch", 22: "s_cmp_eq_u32", 23: "ds_read_b32+v_add"}
 ONLY = ("rc_decode_pow2.hip", "rc_encode.hip")
 
 
@@ -32,7 +35,9 @@ def lib(op):
 def build(ops):
     import __graft_entry__ as g
     for op in ops:
-        g.build_variant(lib(op), ["-DRC_FILL=2", f"-DRC_FILL_OP={op}"], only=ONLY)
+        # (FILL_FLAGS: extra defines, to match the build the fillers are priced against)
+        g.build_variant(lib(op), ["-DRC_DEV_ONLY", "-DRC_FILL=2", f"-DRC_FILL_OP={op}"] +
+                        os.environ.get("FILL_FLAGS", "").split(), only=ONLY)
 
 
 def run(out, ops, rounds):

@@ -120,6 +120,10 @@ def main():
     with open(os.path.join(out, "pmc_calib.json"), "w") as f:
         json.dump({"bytes_per_launch": CAL_BYTES, "shapes": calib}, f, indent=1, sort_keys=True)
 
+    # the library the counters ran on (profile.sh records its sha256 on the box); bench.py
+    # reports roofline.traffic only for that build
+    with open(os.path.join(a.run, "lib.sha256")) as f:
+        lib_sha = f.read().split()[0]
     n_sym = a.chunks * a.chunk_bytes
     alg = bench["roofline"]["alg_bytes_per_launch"]
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
@@ -134,7 +138,8 @@ def main():
         if "SQ_INSTS_VALU" in cs:
             cs["valu_per_wave_symbol"] = cs["SQ_INSTS_VALU"] / (n_sym / 64)
         traffic[f"{a.config}:{a.chunks}:{a.chunk_bytes}:{dom}"] = {
-            "hbm_bytes_per_launch": int(hbm), "round": a.tag, "bytes": {k: int(v) for k, v in b.items()},
+            "hbm_bytes_per_launch": int(hbm), "round": a.tag, "lib_sha256": lib_sha,
+            "bytes": {k: int(v) for k, v in b.items()},
             "correction": "TCC->EA read requests by size (32/64/128 B) + write requests by size "
                           "(= WRITE_SIZE); FETCH_SIZE alone tallies 128-B reads at 64 B"}
     with open(os.path.join(out, "pmc.json"), "w") as f:

@@ -17,6 +17,7 @@ O="$ROOT/gpurun_out/prof_$TAG"
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 cd "$ROOT"
+sha256sum range_coder_rust_amd/librc_amd.so > "$O/lib.sha256"  # (pmc_traffic.py keys traffic.json to it)
 # the PMC passes replay the headline workload once (no Zipf leg, no CPU sample): one launch each
 PMC=(python3 bench.py --no-cpu-baseline --no-zipf --no-adaptive --no-model-build --no-container
      --no-host-stream --steps 1 --warmup 0)
