@@ -35,6 +35,8 @@
 // symbol ahead) and an exact integer correction.
 #include "rc_common.h"
 
+#include <stdlib.h>
+
 #define AWG 64  // one wave per workgroup
 #define TREE_BYTES (255 * 128)
 #define ROW(j) (((j) - 1) * 128)  // byte offset of node j's row
@@ -1005,14 +1007,22 @@ hipError_t rc_adaptive_decode_launch(hipStream_t stream, const AdaptParams& p,
                                      const uint8_t* code, const u64* code_off,
                                      const u64* code_len, uint8_t* syms_out, const u64* sym_off,
                                      u32 n_chunks, u32* flags) {
+  // Measurements only: RC_ADAPT_DEC_LDS=bytes launches
+  // models of <= 128 symbols with that much LDS per wave (>= the 128 rows of nodes 1..128).
+  // Their nodes 129..255 hold zeros: reads past the allocation return 0 and writes to it are
+  // dropped, so the output stays exact while more waves share a CU.
+  size_t lds = TREE_BYTES;
+  if (const char* e = getenv("RC_ADAPT_DEC_LDS")) {
+    const size_t b = (size_t)strtoul(e, nullptr, 10);
+    if (p.n <= 128 && b >= 128 * 128 && b < TREE_BYTES) lds = b;
+  }
   // 256-symbol models keep total >= 256 (every count >= 1), so r < 2^56: 24-bit high products
   if (p.n == 256)
     hipLaunchKernelGGL(k_decode_adaptive<1>, dim3((n_chunks + AWG - 1) / AWG), dim3(AWG),
                        TREE_BYTES, stream, p, code, code_off, code_len, syms_out, sym_off,
                        n_chunks, flags);
   else
-    hipLaunchKernelGGL(k_decode_adaptive<0>, dim3((n_chunks + AWG - 1) / AWG), dim3(AWG),
-                       TREE_BYTES, stream, p, code, code_off, code_len, syms_out, sym_off,
-                       n_chunks, flags);
+    hipLaunchKernelGGL(k_decode_adaptive<0>, dim3((n_chunks + AWG - 1) / AWG), dim3(AWG), lds,
+                       stream, p, code, code_off, code_len, syms_out, sym_off, n_chunks, flags);
   return hipGetLastError();
 }

@@ -39,7 +39,7 @@ typedef u32 u32x3 __attribute__((ext_vector_type(3)));
 #endif
 // the filler register: a VGPR pair for the 64-bit instructions, one VGPR otherwise; the scalar
 // and branch fillers (RC_FILL_OP >= 20) carry an SGPR, the LDS filler a VGPR address
-#if RC_FILL_OP >= 20
+#if RC_FILL_OP >= 20 && RC_FILL_OP < 24
 struct rc_fill_t {
   u32 x;
   __device__ rc_fill_t& operator=(int v) { x = (u32)v; return *this; }
@@ -87,6 +87,11 @@ static __device__ __forceinline__ void rc_filler_one(u32& x) {
     case 12: asm volatile("v_ffbh_u32 %0, %0" : "+v"(x)); break;
     case 13: asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(x)); break;
     case 14: asm volatile("v_cmp_gt_u32_e64 %0, %1, %1" : "=s"(c) : "v"(x)); break;
+    // a compare into VCC and a select reading it, against the same through an SGPR pair (the
+    // pair is the price DESIGN.md §5 gives a VCC read, measured in isolation in round 1)
+    // (with the 2 wait states a VALU read of a VALU-written SGPR needs on gfx950)
+    case 24: asm volatile("v_cmp_lt_u32_e32 vcc, 1, %0\n\ts_nop 1\n\tv_cndmask_b32_e32 %0, 1, %0, vcc" : "+v"(x) : : "vcc"); break;
+    case 25: asm volatile("v_cmp_lt_u32_e64 %1, 1, %0\n\ts_nop 1\n\tv_cndmask_b32_e64 %0, 1, %0, %1" : "+v"(x), "=s"(c)); break;
     case 15: asm volatile("v_mul_f32 %0, %0, %0" : "+v"(x)); break;
     default: asm volatile("v_xor_b32 %0, 1, %0" : "+v"(x)); break;
   }

@@ -38,7 +38,7 @@ static_assert(FLUSH_AT - 1 + 7 * 3 + (8 + 7) <= 4 * ENC_RING - 1,
 // slot mod 4.
 // ENC_ROWS 0 (round 4): column-major, slot j of lane L at dword 64 j + L (stride 256 B).
 #ifndef ENC_ROWS
-#define ENC_ROWS 0  // (1 once measured on the GPU: variants/librc_amd_encrows.so)
+#define ENC_ROWS 1
 #endif
 #define ENC_SLOT_BYTES (ENC_ROWS ? 32u : 256u)  // byte distance between a lane's slots j, j + 1
 // LDS dword index of lane L's column inside its wave's ring
@@ -358,6 +358,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
                                                         u64* __restrict__ out_len,
                                                         u32* __restrict__ flags) {
   RC_STAMP_BEGIN();
+  rc_set_prio(m.prio_step);
   __shared__ uint2 s_tab[256];
   // (1-KiB aligned: a column base has no bits in the row field, ENC_ROWS)
   __shared__ __attribute__((aligned(1024))) u32 s_ring[WAVES * ENC_RING * 64];
@@ -445,6 +446,7 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
     c3 = tp[3];
   }
   for (u64 t = 0; t < tmin; ++t) {
+    rc_prio_rotate(m.prio_rot);
     uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
     if (t + 1 < tmin) {
       const uint4* q = tp + (t + 1) * tstep;
@@ -502,10 +504,13 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
 }
 
 
-hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a, int div, int smv,
+hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a_in, int div, int smv,
                                    const uint8_t* syms, const u64* sym_off, u32 n_chunks,
                                    uint8_t* out, const u64* out_off, u64* out_len, u32* flags) {
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
+  ModelArgs a = a_in;
+  a.prio_step = rc_prio_step(grid.x);
+  a.prio_rot = rc_prio_rot();
 #define RC_ENC_LAUNCH(D, S)                                                                   \
   hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, stream, a, syms, sym_off,      \
                      n_chunks, out, out_off, out_len, flags)

@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <unordered_map>
@@ -75,14 +76,12 @@ static __device__ __forceinline__ u32 settle_count(u64 low, u64 range) {
   return k;
 }
 
-__global__ __launch_bounds__(RWG) void k_stream_encode(
-    rc_stream_state* __restrict__ st, const u32* __restrict__ trip, const u64* __restrict__ sym_off,
-    u32 n_streams, uint8_t* __restrict__ out, const u64* __restrict__ out_off,
+// Encoder::encode x n (+ finish) for stream k (the body of k_stream_encode and of the service)
+static __device__ void stream_encode_one(
+    u32 k, rc_stream_state* __restrict__ st, const u32* __restrict__ trip,
+    const u64* __restrict__ sym_off, uint8_t* __restrict__ out, const u64* __restrict__ out_off,
     u64* __restrict__ out_len, uint8_t* __restrict__ nbytes, u32 finish,
     u32* __restrict__ flags) {
-  const u32 k = blockIdx.x * RWG + threadIdx.x;
-  if (k >= n_streams) return;
-  RC_VGPR_FLOOR_48();
   rc_stream_state S = st[k];
   const u64 s0 = sym_off[k], n = sym_off[k + 1] - s0;
   uint8_t* o = out + out_off[k];
@@ -147,21 +146,24 @@ __global__ __launch_bounds__(RWG) void k_stream_encode(
   flags[k] = S.flags;
 }
 
-__global__ __launch_bounds__(RWG) void k_stream_decode(
-    const u32* __restrict__ c_tab, const u32* __restrict__ cum_tab, u32 n_alpha, u32 total,
-    rc_stream_state* __restrict__ st, const uint8_t* __restrict__ code,
-    const u64* __restrict__ code_off, const u64* __restrict__ code_len,
-    uint8_t* __restrict__ syms, const u64* __restrict__ sym_off, u32 n_streams,
+__global__ __launch_bounds__(RWG) void k_stream_encode(
+    rc_stream_state* __restrict__ st, const u32* __restrict__ trip, const u64* __restrict__ sym_off,
+    u32 n_streams, uint8_t* __restrict__ out, const u64* __restrict__ out_off,
+    u64* __restrict__ out_len, uint8_t* __restrict__ nbytes, u32 finish,
     u32* __restrict__ flags) {
-  __shared__ u32 s_c[256], s_cum[256];
-  for (u32 j = threadIdx.x; j < n_alpha; j += RWG) {
-    s_c[j] = c_tab[j];
-    s_cum[j] = cum_tab[j];
-  }
-  __syncthreads();
   const u32 k = blockIdx.x * RWG + threadIdx.x;
   if (k >= n_streams) return;
-  RC_VGPR_FLOOR_64();
+  RC_VGPR_FLOOR_48();
+  stream_encode_one(k, st, trip, sym_off, out, out_off, out_len, nbytes, finish, flags);
+}
+
+// Decoder::decode x n for stream k against the table in LDS (the body of k_stream_decode and of
+// the service)
+static __device__ void stream_decode_one(
+    u32 k, const u32* s_c, const u32* s_cum, u32 n_alpha, u32 total,
+    rc_stream_state* __restrict__ st, const uint8_t* __restrict__ code,
+    const u64* __restrict__ code_off, const u64* __restrict__ code_len,
+    uint8_t* __restrict__ syms, const u64* __restrict__ sym_off, u32* __restrict__ flags) {
   rc_stream_state S = st[k];
   const uint8_t* cp = code + code_off[k];
   const u64 clen = code_len[k];
@@ -230,6 +232,144 @@ __global__ __launch_bounds__(RWG) void k_stream_decode(
   flags[k] = S.flags;
 }
 
+__global__ __launch_bounds__(RWG) void k_stream_decode(
+    const u32* __restrict__ c_tab, const u32* __restrict__ cum_tab, u32 n_alpha, u32 total,
+    rc_stream_state* __restrict__ st, const uint8_t* __restrict__ code,
+    const u64* __restrict__ code_off, const u64* __restrict__ code_len,
+    uint8_t* __restrict__ syms, const u64* __restrict__ sym_off, u32 n_streams,
+    u32* __restrict__ flags) {
+  __shared__ u32 s_c[256], s_cum[256];
+  for (u32 j = threadIdx.x; j < n_alpha; j += RWG) {
+    s_c[j] = c_tab[j];
+    s_cum[j] = cum_tab[j];
+  }
+  __syncthreads();
+  const u32 k = blockIdx.x * RWG + threadIdx.x;
+  if (k >= n_streams) return;
+  RC_VGPR_FLOOR_64();
+  stream_decode_one(k, s_c, s_cum, n_alpha, total, st, code, code_off, code_len, syms, sym_off,
+                    flags);
+}
+
+// ------------------------------------------------------------------------------------------
+// The stream service: one persistent wave per context that takes the one-stream host calls
+// (rc_stream_encode_host / rc_stream_decode_host) from a mailbox in host memory, so a call is
+// a store of its request block plus a poll, not a copy, a launch, a copy and a stream
+// synchronisation (caller-adaptive Decoder::decode, decoder.rs:38-54, paid a
+// launch and two pinned round trips per symbol).
+//
+// The mailbox is pinned, coherent, device-mapped host memory.  The host writes the request
+// block (the same layout the launch path copies to the device) and then `seq` (release); the
+// wave polls `seq` (system-scope acquire), copies the block into device scratch with all 64
+// lanes, runs the same per-stream body as the launch path on lane 0, copies the result ranges
+// back into the mailbox and sets `ack` (release).  It leaves on `stop`, after SVC_IDLE_MS
+// without a request, or after SVC_LIFE_MS in all, so it never outlives its caller for long: a
+// later call starts a new one (an epoch: `alive` is 2 epoch + 1 while epoch's wave runs and
+// 2 epoch + 2 once it left).  Every exit condition is checked on every poll.
+// ------------------------------------------------------------------------------------------
+#define SVC_IDLE_MS 5
+#define SVC_LIFE_MS 2000
+#define SVC_BLOCK (64u << 10)  // request / result block bytes (larger calls take the launch path)
+enum { SVC_ENCODE = 1, SVC_DECODE = 2 };
+
+struct alignas(64) SvcBox {
+  u32 seq, p0[15];    // host -> wave: request number (written last)
+  u32 ack, p1[15];    // wave -> host: the last request done
+  u32 alive, p2[15];  // wave: 2 epoch + 1 running, 2 epoch + 2 left
+  u32 stop, p3[15];   // host: leave now
+  u32 op, n_alpha, total, finish;
+  u64 in_bytes;               // block bytes the wave reads (a multiple of 16)
+  u64 head_bytes;             // result head [0, head_bytes) copied back (multiple of 16)
+  u64 tail_off, tail_bytes;   // result tail [tail_off, + tail_bytes) copied back (multiples of 16)
+  u64 o[8];                   // byte offsets of the body's arguments inside the block
+  u32 p4[4];
+};
+static_assert(sizeof(SvcBox) == 384, "mailbox header layout");
+
+static __device__ __forceinline__ u32 sys_load(const u32* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// header fields of the current request (vector loads at system scope, after the acquire of seq)
+static __device__ __forceinline__ u32 hdr32(const u32* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+static __device__ __forceinline__ u64 hdr64(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+static __device__ __forceinline__ void sys_store(u32* p, u32 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// copy [off, off + bytes) (16-B multiples) from src to dst with the wave's 64 lanes
+static __device__ __forceinline__ void svc_copy(char* dst, const char* src, u64 off, u64 bytes,
+                                                u32 lane) {
+  for (u64 i = off + 16 * lane; i < off + bytes; i += 16 * RWG)
+    *(u32x4*)(dst + i) = *(const volatile u32x4*)(src + i);
+}
+
+__global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, char* hblk, char* dblk,
+                                                        u32 epoch, u64 idle_ticks,
+                                                        u64 life_ticks) {
+  __shared__ u32 s_c[256], s_cum[256];
+  const u32 lane = threadIdx.x;
+  u32 done = __builtin_amdgcn_readfirstlane(sys_load(&box->ack));
+  if (lane == 0) sys_store(&box->alive, 2 * epoch + 1);
+  const u64 t0 = __builtin_amdgcn_s_memrealtime();
+  u64 tl = t0;
+  for (;;) {
+    const u32 seq = __builtin_amdgcn_readfirstlane(sys_load(&box->seq));
+    const u32 stop = __builtin_amdgcn_readfirstlane(sys_load(&box->stop));
+    const u64 now = __builtin_amdgcn_s_memrealtime();
+    if (stop || now - t0 > life_ticks) break;
+    if (seq == done) {
+      if (now - tl > idle_ticks) break;
+      __builtin_amdgcn_s_sleep(8);
+      continue;
+    }
+    const u32 op = hdr32(&box->op);
+    const u64 in_b = hdr64(&box->in_bytes), head_b = hdr64(&box->head_bytes);
+    const u64 t_off = hdr64(&box->tail_off), t_b = hdr64(&box->tail_bytes);
+    u64 o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = hdr64(&box->o[j]);
+    svc_copy(dblk, hblk, 0, in_b, lane);
+    __threadfence_block();
+    __syncthreads();
+    if (op == SVC_DECODE) {
+      const u32 na = hdr32(&box->n_alpha), tot = hdr32(&box->total);
+      for (u32 j = lane; j < na; j += RWG) {
+        s_c[j] = ((const u32*)(dblk + o[2]))[j];
+        s_cum[j] = ((const u32*)(dblk + o[3]))[j];
+      }
+      __syncthreads();
+      // block: state | offsets (code_off, code_len, sym_off[0..1]) | flags | c | cum | window | syms
+      if (lane == 0)
+        stream_decode_one(0, s_c, s_cum, na, tot, (rc_stream_state*)dblk,
+                          (const uint8_t*)(dblk + o[4]), (const u64*)(dblk + o[0]),
+                          (const u64*)(dblk + o[0] + 8), (uint8_t*)(dblk + o[5]),
+                          (const u64*)(dblk + o[0] + 16), (u32*)(dblk + o[1]));
+    } else if (op == SVC_ENCODE && lane == 0) {
+      // block: state | offsets (sym_off[0..1], out_off[0..1]) | out_len | flags | triples | nb | out
+      stream_encode_one(0, (rc_stream_state*)dblk, (const u32*)(dblk + o[3]),
+                        (const u64*)(dblk + o[0]), (uint8_t*)(dblk + o[5]),
+                        (const u64*)(dblk + o[0] + 16), (u64*)(dblk + o[1]),
+                        o[6] ? (uint8_t*)(dblk + o[4]) : (uint8_t*)nullptr, hdr32(&box->finish),
+                        (u32*)(dblk + o[2]));
+    }
+    __threadfence();
+    __syncthreads();
+    svc_copy(hblk, dblk, 0, head_b, lane);
+    svc_copy(hblk, dblk, t_off, t_b, lane);
+    __threadfence_system();
+    __syncthreads();
+    if (lane == 0) sys_store(&box->ack, seq);
+    done = seq;
+    tl = __builtin_amdgcn_s_memrealtime();
+  }
+  __threadfence_system();
+  if (lane == 0) sys_store(&box->alive, 2 * epoch + 2);
+}
+
 struct Dev {
   int prev = -1;
   explicit Dev(int dev) {
@@ -250,8 +390,10 @@ struct Dev {
 // held under its own mutex for the whole call: the Python mirrors share one default context
 // between threads, and ctypes releases the GIL inside the call.  A call keeps its Stage alive
 // by a shared_ptr, so an rc_ctx_destroy racing with it cannot free the mutex under it; the
-// release marks the block dead, and a call that locks it afterwards fails instead of
-// re-growing a block nobody would free.
+// release marks the block dead, and a call that already held the shared_ptr and locks it
+// afterwards fails instead of re-growing a block nobody would free.  (A call that starts after
+// rc_ctx_destroy uses a destroyed context: a caller contract violation, as with every rc_*
+// entry point.)
 struct Stage {
   std::mutex mu;
   char* host = nullptr;
@@ -296,6 +438,123 @@ char* stage_acquire(const rc_ctx* ctx, size_t bytes, char** dev, std::shared_ptr
 // Above this many worst-case output bytes, rc_stream_encode_host reads back the state first and
 // then only the bytes written (two waits); below it one copy of the whole region is cheaper.
 constexpr u64 kTwoPhaseBytes = 256u << 10;
+
+// The context's stream service (host side): the mailbox, the device scratch, the wave's own
+// non-blocking stream.  Held under its mutex for a whole call, like the staging block.
+struct Svc {
+  std::mutex mu;
+  SvcBox* box = nullptr;  // host address of the mailbox (header, then the block)
+  char* hblk_dev = nullptr;  // device address of the block inside the mailbox
+  char* dblk = nullptr;      // device scratch
+  hipStream_t stream = nullptr;
+  u32 epoch = 0, seq = 0;
+  bool launched = false, dead = false, broken = false;
+};
+std::mutex g_svc_mu;
+std::unordered_map<const rc_ctx*, std::shared_ptr<Svc>> g_svcs;
+// at process exit, tell any running wave to leave (no HIP calls: the runtime may be going too;
+// a wave leaves within one poll, and by SVC_IDLE_MS in any case)
+struct SvcAtExit {
+  ~SvcAtExit() {
+    std::lock_guard<std::mutex> g(g_svc_mu);
+    for (auto& kv : g_svcs)
+      if (kv.second && kv.second->box) __atomic_store_n(&kv.second->box->stop, 1u, __ATOMIC_RELEASE);
+  }
+} g_svc_at_exit;
+
+// RC_STREAM_SERVICE=0 sends every call down the launch path (read at every call, so tests can
+// switch it between calls; a getenv is ~0.1 us)
+bool svc_enabled() {
+  const char* e = getenv("RC_STREAM_SERVICE");
+  return !(e && e[0] == '0');
+}
+
+std::shared_ptr<Svc> svc_get(const rc_ctx* ctx) {
+  std::lock_guard<std::mutex> g(g_svc_mu);
+  auto& slot = g_svcs[ctx];
+  if (!slot) slot = std::make_shared<Svc>();
+  return slot;
+}
+
+// stop the wave (if any) and free everything; the caller holds sv->mu
+void svc_teardown(Svc* sv) {
+  if (sv->box) {
+    __atomic_store_n(&sv->box->stop, 1u, __ATOMIC_RELEASE);
+    if (sv->stream) (void)hipStreamSynchronize(sv->stream);
+  }
+  if (sv->stream) (void)hipStreamDestroy(sv->stream);
+  if (sv->box) (void)hipHostFree(sv->box);
+  if (sv->dblk) (void)hipFree(sv->dblk);
+  sv->stream = nullptr;
+  sv->box = nullptr;
+  sv->dblk = nullptr;
+  sv->hblk_dev = nullptr;
+  sv->launched = false;
+}
+
+// One request through the service.  fill(h) writes the request block at h (in the mailbox) and
+// the header fields; after the wave acknowledged it, the results are in the same block.
+// Returns false (and the call takes the launch path) when the service is off, broken, or
+// cannot be set up; RC_E_DEVICE in *err when the wave did not answer.
+template <class Fill>
+bool svc_call(const rc_ctx* ctx, Svc* sv, Fill fill, rc_status* err) {
+  if (sv->dead || sv->broken) return false;
+  if (!sv->box) {
+    void* hb = nullptr;
+    if (hipHostMalloc(&hb, sizeof(SvcBox) + SVC_BLOCK,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+      sv->broken = true;
+      return false;
+    }
+    memset(hb, 0, sizeof(SvcBox));
+    sv->box = (SvcBox*)hb;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, hb, 0) != hipSuccess ||
+        hipMalloc((void**)&sv->dblk, SVC_BLOCK) != hipSuccess ||
+        hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess) {
+      svc_teardown(sv);
+      sv->broken = true;
+      return false;
+    }
+    sv->hblk_dev = (char*)dp + sizeof(SvcBox);
+  }
+  SvcBox* b = sv->box;
+  fill((char*)(b + 1), b);
+  const u32 s = ++sv->seq;
+  __atomic_store_n(&b->seq, s, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (u32 spin = 0;; ++spin) {
+    if (__atomic_load_n(&b->ack, __ATOMIC_ACQUIRE) == s) return true;
+    // no wave of the current epoch running: start one (it takes the pending request)
+    if (!sv->launched || __atomic_load_n(&b->alive, __ATOMIC_ACQUIRE) == 2 * sv->epoch + 2) {
+      ++sv->epoch;
+      hipLaunchKernelGGL(k_stream_service, dim3(1), dim3(RWG), 0, sv->stream, (SvcBox*)(sv->hblk_dev - sizeof(SvcBox)),
+                         sv->hblk_dev, sv->dblk, sv->epoch, (u64)SVC_IDLE_MS * 100000ull,
+                         (u64)SVC_LIFE_MS * 100000ull);
+      if (hipGetLastError() != hipSuccess) {
+        sv->broken = true;
+        *err = RC_E_DEVICE;
+        return true;
+      }
+      sv->launched = true;
+    }
+    if ((spin & 1023) == 1023) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+        svc_teardown(sv);  // (waits for the wave to leave: every exit is bounded)
+        sv->broken = true;
+        *err = RC_E_DEVICE;
+        return true;
+      }
+      if (hipStreamQuery(sv->stream) != hipSuccess &&
+          hipStreamQuery(sv->stream) != hipErrorNotReady) {
+        sv->broken = true;
+        *err = RC_E_DEVICE;
+        return true;
+      }
+    }
+    __builtin_ia32_pause();
+  }
+}
 
 }  // namespace
 
@@ -355,6 +614,42 @@ rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint3
   // block: state | offsets (4 x u64) | out_len | flags | triples || nbytes | out
   const size_t o_off = 64, o_len = o_off + 32, o_fl = o_len + 16, o_tr = o_fl + 16;
   const size_t o_nb = o_tr + ((12 * n + 15) & ~15ull), o_out = o_nb + ((n + 15) & ~15ull);
+  const size_t tail = (o_out + need - o_nb + 15) & ~15ull;
+  if (svc_enabled() && o_nb + tail <= SVC_BLOCK) {  // a small call: through the stream service
+    auto sv = svc_get(ctx);
+    std::lock_guard<std::mutex> slk(sv->mu);
+    rc_status err = RC_OK;
+    if (svc_call(ctx, sv.get(), [&](char* h, SvcBox* b) {
+          memcpy(h, state, sizeof *state);
+          const u64 offs[4] = {0, n, 0, need};
+          memcpy(h + o_off, offs, sizeof offs);
+          if (n) memcpy(h + o_tr, triples, 12 * n);
+          b->op = SVC_ENCODE;
+          b->finish = finish;
+          b->in_bytes = o_nb;
+          b->head_bytes = o_tr;
+          b->tail_off = o_nb;
+          b->tail_bytes = tail;
+          const u64 o[8] = {o_off, o_len, o_fl, o_tr, o_nb, o_out, nbytes ? 1u : 0u, 0};
+          memcpy(b->o, o, sizeof o);
+        }, &err)) {
+      if (err != RC_OK) return err;
+      const char* h = (const char*)(sv->box + 1);
+      rc_stream_state nst;
+      memcpy(&nst, h, sizeof nst);
+      u64 w;
+      u32 fl;
+      memcpy(&w, h + o_len, 8);
+      memcpy(&fl, h + o_fl, 4);
+      if (w > need || nst.n - state->n > n) return RC_E_DEVICE;
+      if (w) memcpy(out, h + o_out, w);
+      if (nbytes && n) memcpy(nbytes, h + o_nb, nst.n - state->n);
+      *state = nst;
+      *out_len = w;
+      if (flags_out) *flags_out = fl;
+      return fl ? RC_E_CHUNK : RC_OK;
+    }
+  }
   char* d = nullptr;
   std::shared_ptr<Stage> keep;
   std::unique_lock<std::mutex> lk;
@@ -424,6 +719,45 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
   // block: state | offsets: code_off, code_len, sym_off[0..1] | flags | c | cum | window || syms
   const size_t o_off = 64, o_fl = o_off + 32, o_c = o_fl + 16, o_cum = o_c + 1024;
   const size_t o_win = o_cum + 1024, o_sym = o_win + ((wlen + 15) & ~15ull);
+  const size_t tail = (n + 15) & ~15ull;
+  if (svc_enabled() && o_sym + tail <= SVC_BLOCK) {  // a small call: through the stream service
+    auto sv = svc_get(ctx);
+    std::lock_guard<std::mutex> slk(sv->mu);
+    rc_status err = RC_OK;
+    if (svc_call(ctx, sv.get(), [&](char* h, SvcBox* b) {
+          rc_stream_state rel = *state;
+          rel.pos -= p0;  // the window starts at p0 (stage 0: at the stream start)
+          memcpy(h, &rel, sizeof rel);
+          const u64 offs[4] = {0, wlen, 0, n};
+          memcpy(h + o_off, offs, sizeof offs);
+          memcpy(h + o_c, c, 4ull * n_symbols);
+          memcpy(h + o_cum, cum, 4ull * n_symbols);
+          if (wlen) memcpy(h + o_win, code + p0, wlen);
+          b->op = SVC_DECODE;
+          b->n_alpha = n_symbols;
+          b->total = total_freq;
+          b->in_bytes = o_sym;
+          b->head_bytes = o_c;
+          b->tail_off = o_sym;
+          b->tail_bytes = tail;
+          const u64 o[8] = {o_off, o_fl, o_c, o_cum, o_win, o_sym, 0, 0};
+          memcpy(b->o, o, sizeof o);
+        }, &err)) {
+      if (err != RC_OK) return err;
+      const char* h = (const char*)(sv->box + 1);
+      rc_stream_state nst;
+      u32 fl;
+      memcpy(&nst, h, sizeof nst);
+      memcpy(&fl, h + o_fl, 4);
+      const u64 got = nst.n - state->n;
+      if (got > n) return RC_E_DEVICE;
+      if (got) memcpy(syms, h + o_sym, got);
+      nst.pos += p0;
+      *state = nst;
+      if (flags_out) *flags_out = fl;
+      return fl ? RC_E_CHUNK : RC_OK;
+    }
+  }
   char* d = nullptr;
   std::shared_ptr<Stage> keep;
   std::unique_lock<std::mutex> lk;
@@ -464,6 +798,22 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
 
 // internal: free the context's staging block (called by rc_ctx_destroy)
 void rc_resume_release_(const rc_ctx* ctx) {
+  {  // the stream service: stop its wave, free the mailbox
+    std::shared_ptr<Svc> sv;
+    {
+      std::lock_guard<std::mutex> lk(g_svc_mu);
+      auto it = g_svcs.find(ctx);
+      if (it != g_svcs.end()) {
+        sv = std::move(it->second);
+        g_svcs.erase(it);
+      }
+    }
+    if (sv) {
+      std::lock_guard<std::mutex> lk(sv->mu);
+      svc_teardown(sv.get());
+      sv->dead = true;
+    }
+  }
   std::shared_ptr<Stage> st;
   {
     std::lock_guard<std::mutex> lk(g_stage_mu);

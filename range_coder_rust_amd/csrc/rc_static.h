@@ -22,6 +22,8 @@
 #pragma once
 #include "rc_common.h"
 
+#include <stdlib.h>
+
 #define WG 256
 #define WAVES (WG / 64)
 #define ENC_RING 32          // dwords per lane in the encoder's output ring (128 B)
@@ -92,7 +94,54 @@ struct ModelArgs {
   u32 la_mask;
   float la_magic;    // 1.5 * 2^(23 + la_shift): fma(X, G, la_magic)'s low bits are q >> la_shift
   double inv_up;     // 1 / total rounded up (small models, DIV_MAGIC: range / total in f64)
+  u32 prio_step;     // set per launch: workgroup b runs at s_setprio min(3, b / prio_step)
+                     // (0: all at priority 0; rc_prio_step)
+  u32 prio_rot;      // set per launch: 0, or rotate priorities every 2^prio_rot ticks of the
+                     // 100 MHz clock (rc_prio_rotate)
 };
+
+// Wave priority by dispatch order ("the end of a launch").  Every chunk is one
+// lane's serial stream and the chunks are of equal length, so a launch ends with a ramp-down
+// in which the waves dispatched last run with fewer and fewer partners per SIMD.  Issue is
+// arbitrated by priority, then age: at equal priority the oldest wave of a SIMD runs nearly
+// unimpeded and the youngest takes the leftover slots, which stretches the end.  A later
+// workgroup at a higher priority catches up instead.  Scratch control (read at every launch):
+// RC_PRIO_STEP=k sets prio_step = k; RC_PRIO_LAST=n gives the last n workgroups priority 1.
+static inline u32 rc_prio_step(u32 grid) {
+  const char* e = getenv("RC_PRIO_STEP");
+  if (e && *e) return (u32)strtoul(e, nullptr, 10);
+  e = getenv("RC_PRIO_LAST");
+  if (e && *e) {
+    const u32 n = (u32)strtoul(e, nullptr, 10);
+    return n && n < grid ? grid - n : 0u;
+  }
+  return 0u;
+}
+// RC_PRIO_ROT=k: every 64 symbols a wave sets its priority to ((t >> k) + its wave slot) mod 4,
+// t = s_memrealtime.  The waves of a SIMD hold distinct slots (HW_ID wave id), so at any time
+// they hold different priorities and each takes every priority in turn: issue goes round-robin
+// at 2^k x 10 ns granularity instead of oldest-first, and waves that started together stay
+// together (at 4 waves per SIMD and 16 waves per SIMD in all, four even rounds).
+static inline u32 rc_prio_rot() {
+  const char* e = getenv("RC_PRIO_ROT");
+  return e && *e ? (u32)strtoul(e, nullptr, 10) : 0u;
+}
+static __device__ __forceinline__ void rc_prio_rotate(u32 k) {
+  if (!k) return;
+  const u32 t = (u32)(__builtin_amdgcn_s_memrealtime() >> k);
+  const u32 p = (t + __builtin_amdgcn_s_getreg(0xF804)) & 3u;  // HW_ID bits 3:0: wave slot
+  if (p == 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+static __device__ __forceinline__ void rc_set_prio(u32 step) {
+  if (!step) return;
+  const u32 p = __builtin_amdgcn_readfirstlane(blockIdx.x / step);
+  if (p >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+}
 
 // Small bucket models (k_decode_static LUT 4: 2048 < total <= 2^16; the pair decoder, LUT 3, is
 // opt-in, RC_DEC_PAIR).  LDS

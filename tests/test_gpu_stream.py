@@ -534,3 +534,72 @@ def test_threads_share_the_default_context(ctx):
         f, b, _ = cpu.encode(c, cum, tables[k].total, np.asarray(streams[k], np.uint8))
         assert f == 0 and bytes(codes[k]) == bytes(b), k
         assert decoded[k] == streams[k], k
+
+
+# ---- the stream service (rc_resume.hip): small host calls through a persistent wave ----------
+
+def _adaptive_round_trip(ctx_, n=1500, seed=11):
+    syms = _zipfish(n, seed)
+    m = AdaptiveFreqTable(256, 32, 4000, 64)
+    enc = rc.Encoder(ctx=ctx_)
+    rets = []
+    for i, s in enumerate(syms):
+        rets.append(enc.encode(m, s))
+        m.update(s, i)
+        if i % 97 == 0:
+            enc.peek_code()  # a flush: one small encode call
+    code = enc.finish()
+    m = AdaptiveFreqTable(256, 32, 4000, 64)
+    dec = rc.Decoder(code, ctx=ctx_)
+    out = []
+    for i in range(n):
+        s = dec.decode(m)  # the table changes every symbol: one decode call per symbol
+        out.append(s)
+        m.update(s, i)
+    return syms, code, [int(r) for r in rets], out
+
+
+@pytest.mark.parametrize("service", ["1", "0"])
+def test_service_and_launch_paths_vs_reference(ctx, monkeypatch, service):
+    """The same caller-adaptive round trip through the service (default) and through the
+    launch path (RC_STREAM_SERVICE=0), against ref_literal's bytes and encode() counts."""
+    monkeypatch.setenv("RC_STREAM_SERVICE", service)
+    syms, code, rets, out = _adaptive_round_trip(ctx)
+    assert code == R.encode_adaptive_stream(256, 32, 4000, 64, syms)
+    ref = R.Encoder()
+    ref_m = R.AdaptiveModel(256, 32, 4000, 64)
+    want = []
+    for i, s in enumerate(syms):
+        want.append(ref.encode(ref_m, s))
+        ref_m.update(s, i)
+    assert rets == want
+    assert out == syms
+
+
+def test_service_restarts_after_idle_and_stops_on_destroy(ctx, monkeypatch):
+    """The wave leaves after its idle time; the next call starts a new one.  rc_ctx_destroy
+    with a wave running returns promptly, and torch.cuda.synchronize() is not held up for
+    longer than the idle time."""
+    import time
+    monkeypatch.setenv("RC_STREAM_SERVICE", "1")
+    c2 = rc.Context(0)
+    try:
+        sd = _sample_table()
+        for rep in range(3):
+            enc = rc.Encoder(ctx=c2)
+            for i in SAMPLE:
+                enc.encode(sd, i)
+            assert enc.finish().hex() == "64475f8970365a2f83b20246c0"
+            dec = rc.Decoder(bytes.fromhex("64475f8970365a2f83b20246c0"), ctx=c2)
+            assert [dec.decode(sd) for _ in SAMPLE] == SAMPLE
+            time.sleep(0.02)  # > the idle time: the wave has left, the next call relaunches
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t0 < 1.0
+        enc = rc.Encoder(ctx=c2)
+        enc.encode(sd, 1)
+        enc.peek_code()  # a wave is running now
+    finally:
+        t0 = time.perf_counter()
+        c2.close()
+        assert time.perf_counter() - t0 < 1.0

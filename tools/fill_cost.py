@@ -24,7 +24,8 @@ OPS = {0: "v_add_u32", 1: "v_lshrrev_b32", 2: "v_lshlrev_b64", 3: "v_mad_u64_u32
        13: "v_lshlrev_b32", 16: "v_lshrrev_b64",
        # round 5: the non-VALU classes (rc_common.h): scalar ALU, a compare + conditional branch,
        # the compare alone, and one LDS read whose result a VALU add waits for
-       20: "s_add_u32", 21: "s_cmp+s_cbranch", 22: "s_cmp_eq_u32", 23: "ds_read_b32+v_add"}
+       20: "s_add_u32", 21: "s_cmp+s_cbranch", 22: "s_cmp_eq_u32", 23: "ds_read_b32+v_add",
+       24: "v_cmp vcc+v_cndmask vcc", 25: "v_cmp+v_cndmask sgpr"}
 ONLY = ("rc_decode_pow2.hip", "rc_encode.hip")
 
 
