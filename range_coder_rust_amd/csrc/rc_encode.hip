@@ -2,6 +2,10 @@
 // notes shared with the decoder).
 #include "rc_static.h"
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 // ------------------------------------------------------------------------------------------
 // Encoder
 //
@@ -45,6 +49,13 @@ static_assert(FLUSH_AT - 1 + 7 * 3 + (8 + 7) <= 4 * ENC_RING - 1,
 static __device__ __forceinline__ u32 ring_col(u32 L) {
   return ENC_ROWS ? (L >> 3) * 256u + (L & 7u) : L;
 }
+#ifndef ENC_TILE_Q
+#define ENC_TILE_Q 4  // 16-B blocks per symbol load (4: 64-B bursts, one 64-symbol tile)
+#endif
+#ifndef ENC_WAVES
+#define ENC_WAVES 4   // waves per SIMD the register allocation must allow
+#endif
+static_assert(ENC_TILE_Q == 4 || ENC_TILE_Q == 2, "tiles of 64 or 32 symbols");
 #define SINK_SLOTS 65536
 __device__ uint4 g_sink[SINK_SLOTS];  // dummy symbol tiles of dead lanes (contents irrelevant)
 RC_STAMP_DEFINE(enc)  // (scratch -DRC_STAMP builds only)
@@ -351,14 +362,14 @@ static __device__ u32 enc_first_error(const ModelArgs& m, const uint8_t* sp, u64
 }
 
 template <int DIV, int SM>
-__global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint8_t* __restrict__ syms,
+__global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, const uint8_t* __restrict__ syms,
                                                         const u64* __restrict__ sym_off,
                                                         u32 n_chunks, uint8_t* __restrict__ out,
                                                         const u64* __restrict__ out_off,
                                                         u64* __restrict__ out_len,
                                                         u32* __restrict__ flags) {
   RC_STAMP_BEGIN();
-  rc_set_prio(m.prio_step);
+  rc_set_prio(m);
   __shared__ uint2 s_tab[256];
   // (1-KiB aligned: a column base has no bits in the row field, ENC_ROWS)
   __shared__ __attribute__((aligned(1024))) u32 s_ring[WAVES * ENC_RING * 64];
@@ -376,7 +387,9 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
   const u32 lane = tid & 63, wave = tid >> 6;
   const u32 k = blockIdx.x * WG + tid;
   const bool live = k < n_chunks;  // dead lanes still take part in the wave's flush rounds
+#if ENC_WAVES == 4
   RC_VGPR_FLOOR_128();
+#endif
 
   u64 s0 = 0, n = 0, o0 = 0, o1 = 0;
   if (live) {
@@ -437,32 +450,32 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
                    __builtin_amdgcn_readfirstlane((u32)tm);  // wave-uniform (scalar) trip count
   const uint4* tp = live ? reinterpret_cast<const uint4*>(sp + head)
                          : reinterpret_cast<const uint4*>(g_sink);
-  const u64 tstep = live ? 4 : 0;  // uint4s per tile
-  uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0;
-  if (tmin) {
-    c0 = tp[0];
-    c1 = tp[1];
-    c2 = tp[2];
-    c3 = tp[3];
+  // loads of ENC_TILE_Q 16-B blocks per lane, the next one in flight while the current one is
+  // coded (ENC_TILE_Q 2: 32 registers fewer, for 5 waves per SIMD; scratch builds)
+  constexpr u32 TQ = ENC_TILE_Q;
+  const u64 tstep = live ? TQ : 0;  // uint4s per load
+  const u64 trips = tmin * (4 / TQ);
+  uint4 c[TQ];
+#pragma unroll
+  for (u32 q = 0; q < TQ; ++q) c[q] = make_uint4(0, 0, 0, 0);
+  if (trips) {
+#pragma unroll
+    for (u32 q = 0; q < TQ; ++q) c[q] = tp[q];
   }
-  for (u64 t = 0; t < tmin; ++t) {
+  for (u64 t = 0; t < trips; ++t) {
     rc_prio_rotate(m.prio_rot);
-    uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
-    if (t + 1 < tmin) {
-      const uint4* q = tp + (t + 1) * tstep;
-      n0 = q[0];
-      n1 = q[1];
-      n2 = q[2];
-      n3 = q[3];
+    uint4 nx[TQ];
+#pragma unroll
+    for (u32 q = 0; q < TQ; ++q) nx[q] = c[q];
+    if (t + 1 < trips) {
+      const uint4* qp = tp + (t + 1) * tstep;
+#pragma unroll
+      for (u32 q = 0; q < TQ; ++q) nx[q] = qp[q];
     }
-    enc16<DIV, SM>(e, m, s_tab, c0, true, lane, wring, wout);
-    enc16<DIV, SM>(e, m, s_tab, c1, true, lane, wring, wout);
-    enc16<DIV, SM>(e, m, s_tab, c2, true, lane, wring, wout);
-    enc16<DIV, SM>(e, m, s_tab, c3, true, lane, wring, wout);
-    c0 = n0;
-    c1 = n1;
-    c2 = n2;
-    c3 = n3;
+#pragma unroll
+    for (u32 q = 0; q < TQ; ++q) enc16<DIV, SM>(e, m, s_tab, c[q], true, lane, wring, wout);
+#pragma unroll
+    for (u32 q = 0; q < TQ; ++q) c[q] = nx[q];
   }
   // body, part 2 (ragged waves): the remaining 16-symbol blocks of the tiles, lanes masked
   const u64 nblk = ntile * 4;
@@ -504,30 +517,47 @@ __global__ __launch_bounds__(WG, 4) void k_encode_static(ModelArgs m, const uint
 }
 
 
+u32 rc_resident_wgs(const void* kernel, int block, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, const void*, size_t>, u32> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> g(mu);
+  const auto key = std::make_tuple(dev, kernel, lds);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return cache[key] = (u32)(per_cu * cus);
+}
+
 hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a_in, int div, int smv,
                                    const uint8_t* syms, const u64* sym_off, u32 n_chunks,
                                    uint8_t* out, const u64* out_off, u64* out_len, u32* flags) {
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
   ModelArgs a = a_in;
-  a.prio_step = rc_prio_step(grid.x);
-  a.prio_rot = rc_prio_rot();
-#define RC_ENC_LAUNCH(D, S)                                                                   \
-  hipLaunchKernelGGL((k_encode_static<D, S>), grid, block, 0, stream, a, syms, sym_off,      \
-                     n_chunks, out, out_off, out_len, flags)
+  // (the launch's wave priorities: rc_static.h)
+  auto go = [&](auto kern) {
+    rc_prio_policy(a, kPrioEncoder, grid.x,
+                   rc_resident_wgs(reinterpret_cast<const void*>(kern), WG, 0));
+    hipLaunchKernelGGL(kern, grid, block, 0, stream, a, syms, sym_off, n_chunks, out, out_off,
+                       out_len, flags);
+  };
 #ifdef RC_DEV_ONLY  // scratch builds for kernel tuning: the headline variants only
   if (div != DIV_POW2 || smv == 0) return hipErrorInvalidValue;
-  if (smv == 2) RC_ENC_LAUNCH(DIV_POW2, 2); else RC_ENC_LAUNCH(DIV_POW2, 1);
+  if (smv == 2) go(k_encode_static<DIV_POW2, 2>); else go(k_encode_static<DIV_POW2, 1>);
 #else
   if (div == DIV_POW2) {
-    if (smv == 2) RC_ENC_LAUNCH(DIV_POW2, 2);
-    else if (smv == 1) RC_ENC_LAUNCH(DIV_POW2, 1);
-    else RC_ENC_LAUNCH(DIV_POW2, 0);
+    if (smv == 2) go(k_encode_static<DIV_POW2, 2>);
+    else if (smv == 1) go(k_encode_static<DIV_POW2, 1>);
+    else go(k_encode_static<DIV_POW2, 0>);
   } else {
-    if (smv == 2) RC_ENC_LAUNCH(DIV_MAGIC, 2);
-    else if (smv == 1) RC_ENC_LAUNCH(DIV_MAGIC, 1);
-    else RC_ENC_LAUNCH(DIV_MAGIC, 0);
+    if (smv == 2) go(k_encode_static<DIV_MAGIC, 2>);
+    else if (smv == 1) go(k_encode_static<DIV_MAGIC, 1>);
+    else go(k_encode_static<DIV_MAGIC, 0>);
   }
 #endif
-#undef RC_ENC_LAUNCH
   return hipGetLastError();
 }

@@ -19,6 +19,7 @@
 // u64 products wrap (release-build semantics of the reference).
 #include "rc_common.h"
 
+#include <stddef.h>
 #include <string.h>
 
 #include <algorithm>
@@ -307,11 +308,24 @@ static __device__ __forceinline__ void svc_copy(char* dst, const char* src, u64 
     *(u32x4*)(dst + i) = *(const volatile u32x4*)(src + i);
 }
 
-__global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, char* hblk, char* dblk,
-                                                        u32 epoch, u64 idle_ticks,
-                                                        u64 life_ticks) {
+#define SVC_BURST 4096u  // bytes of the mailbox read in one burst (header + the block's start)
+// field at byte `off` of the burst held by the lanes (lane l holds bytes 16 (l + 64 j) ..)
+static __device__ __forceinline__ u32 burst32(const u32x4* v, u32 off) {
+  const u32x4& q = v[off / 1024];
+  const u32 w = (off / 4) % 4;
+  const u32 x = w == 0 ? q.x : w == 1 ? q.y : w == 2 ? q.z : q.w;
+  return __builtin_amdgcn_readlane(x, (off / 16) % 64);
+}
+static __device__ __forceinline__ u64 burst64(const u32x4* v, u32 off) {
+  return ((u64)burst32(v, off + 4) << 32) | burst32(v, off);
+}
+
+__global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, char* dbox, u32 epoch,
+                                                        u64 idle_ticks, u64 life_ticks) {
   __shared__ u32 s_c[256], s_cum[256];
   const u32 lane = threadIdx.x;
+  char* const hbox = (char*)box;
+  char* const dblk = dbox + sizeof(SvcBox);
   u32 done = __builtin_amdgcn_readfirstlane(sys_load(&box->ack));
   if (lane == 0) sys_store(&box->alive, 2 * epoch + 1);
   const u64 t0 = __builtin_amdgcn_s_memrealtime();
@@ -323,20 +337,32 @@ __global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, char* hblk,
     if (stop || now - t0 > life_ticks) break;
     if (seq == done) {
       if (now - tl > idle_ticks) break;
-      __builtin_amdgcn_s_sleep(8);
+      __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    const u32 op = hdr32(&box->op);
-    const u64 in_b = hdr64(&box->in_bytes), head_b = hdr64(&box->head_bytes);
-    const u64 t_off = hdr64(&box->tail_off), t_b = hdr64(&box->tail_bytes);
+    // The request in one burst: the first 4 KiB of the mailbox (header and block), every load
+    // in flight before the first is used, so a one-symbol call costs one PCIe round trip; the
+    // header fields come out of the lanes' registers.  (Plain loads: the acquire of seq orders
+    // them after the host's stores.)
+    u32x4 v[SVC_BURST / 1024];
+#pragma unroll
+    for (u32 j = 0; j < SVC_BURST / 1024; ++j) v[j] = *(const u32x4*)(hbox + 16 * (lane + 64 * j));
+    const u32 op = burst32(v, offsetof(SvcBox, op));
+    const u64 in_b = burst64(v, offsetof(SvcBox, in_bytes));
+    const u64 head_b = burst64(v, offsetof(SvcBox, head_bytes));
+    const u64 t_off = burst64(v, offsetof(SvcBox, tail_off));
+    const u64 t_b = burst64(v, offsetof(SvcBox, tail_bytes));
     u64 o[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = hdr64(&box->o[j]);
-    svc_copy(dblk, hblk, 0, in_b, lane);
+    for (int j = 0; j < 8; ++j) o[j] = burst64(v, offsetof(SvcBox, o) + 8 * j);
+#pragma unroll
+    for (u32 j = 0; j < SVC_BURST / 1024; ++j) *(u32x4*)(dbox + 16 * (lane + 64 * j)) = v[j];
+    if (sizeof(SvcBox) + in_b > SVC_BURST)
+      svc_copy(dbox, hbox, SVC_BURST, sizeof(SvcBox) + in_b - SVC_BURST, lane);
     __threadfence_block();
     __syncthreads();
     if (op == SVC_DECODE) {
-      const u32 na = hdr32(&box->n_alpha), tot = hdr32(&box->total);
+      const u32 na = burst32(v, offsetof(SvcBox, n_alpha)), tot = burst32(v, offsetof(SvcBox, total));
       for (u32 j = lane; j < na; j += RWG) {
         s_c[j] = ((const u32*)(dblk + o[2]))[j];
         s_cum[j] = ((const u32*)(dblk + o[3]))[j];
@@ -348,16 +374,19 @@ __global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, char* hblk,
                           (const uint8_t*)(dblk + o[4]), (const u64*)(dblk + o[0]),
                           (const u64*)(dblk + o[0] + 8), (uint8_t*)(dblk + o[5]),
                           (const u64*)(dblk + o[0] + 16), (u32*)(dblk + o[1]));
-    } else if (op == SVC_ENCODE && lane == 0) {
+    } else if (op == SVC_ENCODE) {
+      const u32 fin = burst32(v, offsetof(SvcBox, finish));
       // block: state | offsets (sym_off[0..1], out_off[0..1]) | out_len | flags | triples | nb | out
-      stream_encode_one(0, (rc_stream_state*)dblk, (const u32*)(dblk + o[3]),
-                        (const u64*)(dblk + o[0]), (uint8_t*)(dblk + o[5]),
-                        (const u64*)(dblk + o[0] + 16), (u64*)(dblk + o[1]),
-                        o[6] ? (uint8_t*)(dblk + o[4]) : (uint8_t*)nullptr, hdr32(&box->finish),
-                        (u32*)(dblk + o[2]));
+      if (lane == 0)
+        stream_encode_one(0, (rc_stream_state*)dblk, (const u32*)(dblk + o[3]),
+                          (const u64*)(dblk + o[0]), (uint8_t*)(dblk + o[5]),
+                          (const u64*)(dblk + o[0] + 16), (u64*)(dblk + o[1]),
+                          o[6] ? (uint8_t*)(dblk + o[4]) : (uint8_t*)nullptr, fin,
+                          (u32*)(dblk + o[2]));
     }
     __threadfence();
     __syncthreads();
+    char* const hblk = hbox + sizeof(SvcBox);
     svc_copy(hblk, dblk, 0, head_b, lane);
     svc_copy(hblk, dblk, t_off, t_b, lane);
     __threadfence_system();
@@ -444,8 +473,8 @@ constexpr u64 kTwoPhaseBytes = 256u << 10;
 struct Svc {
   std::mutex mu;
   SvcBox* box = nullptr;  // host address of the mailbox (header, then the block)
-  char* hblk_dev = nullptr;  // device address of the block inside the mailbox
-  char* dblk = nullptr;      // device scratch
+  SvcBox* dbox_host = nullptr;  // device address of the mailbox (mapped host memory)
+  char* dbox = nullptr;         // device scratch mirroring the mailbox (header + block)
   hipStream_t stream = nullptr;
   u32 epoch = 0, seq = 0;
   bool launched = false, dead = false, broken = false;
@@ -484,11 +513,11 @@ void svc_teardown(Svc* sv) {
   }
   if (sv->stream) (void)hipStreamDestroy(sv->stream);
   if (sv->box) (void)hipHostFree(sv->box);
-  if (sv->dblk) (void)hipFree(sv->dblk);
+  if (sv->dbox) (void)hipFree(sv->dbox);
   sv->stream = nullptr;
   sv->box = nullptr;
-  sv->dblk = nullptr;
-  sv->hblk_dev = nullptr;
+  sv->dbox = nullptr;
+  sv->dbox_host = nullptr;
   sv->launched = false;
 }
 
@@ -510,13 +539,13 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, Fill fill, rc_status* err) {
     sv->box = (SvcBox*)hb;
     void* dp = nullptr;
     if (hipHostGetDevicePointer(&dp, hb, 0) != hipSuccess ||
-        hipMalloc((void**)&sv->dblk, SVC_BLOCK) != hipSuccess ||
+        hipMalloc((void**)&sv->dbox, sizeof(SvcBox) + SVC_BLOCK) != hipSuccess ||
         hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess) {
       svc_teardown(sv);
       sv->broken = true;
       return false;
     }
-    sv->hblk_dev = (char*)dp + sizeof(SvcBox);
+    sv->dbox_host = (SvcBox*)dp;
   }
   SvcBox* b = sv->box;
   fill((char*)(b + 1), b);
@@ -528,8 +557,8 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, Fill fill, rc_status* err) {
     // no wave of the current epoch running: start one (it takes the pending request)
     if (!sv->launched || __atomic_load_n(&b->alive, __ATOMIC_ACQUIRE) == 2 * sv->epoch + 2) {
       ++sv->epoch;
-      hipLaunchKernelGGL(k_stream_service, dim3(1), dim3(RWG), 0, sv->stream, (SvcBox*)(sv->hblk_dev - sizeof(SvcBox)),
-                         sv->hblk_dev, sv->dblk, sv->epoch, (u64)SVC_IDLE_MS * 100000ull,
+      hipLaunchKernelGGL(k_stream_service, dim3(1), dim3(RWG), 0, sv->stream, sv->dbox_host,
+                         sv->dbox, sv->epoch, (u64)SVC_IDLE_MS * 100000ull,
                          (u64)SVC_LIFE_MS * 100000ull);
       if (hipGetLastError() != hipSuccess) {
         sv->broken = true;

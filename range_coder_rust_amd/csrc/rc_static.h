@@ -23,6 +23,7 @@
 #include "rc_common.h"
 
 #include <stdlib.h>
+#include <string.h>
 
 #define WG 256
 #define WAVES (WG / 64)
@@ -94,37 +95,68 @@ struct ModelArgs {
   u32 la_mask;
   float la_magic;    // 1.5 * 2^(23 + la_shift): fma(X, G, la_magic)'s low bits are q >> la_shift
   double inv_up;     // 1 / total rounded up (small models, DIV_MAGIC: range / total in f64)
-  u32 prio_step;     // set per launch: workgroup b runs at s_setprio min(3, b / prio_step)
-                     // (0: all at priority 0; rc_prio_step)
+  u32 prio_base;     // set per launch (rc_prio_policy): workgroup b >= prio_base runs at
+  u32 prio_step;     //   s_setprio min(3, 1 + (b - prio_base) / prio_step); ~0: all at 0
   u32 prio_rot;      // set per launch: 0, or rotate priorities every 2^prio_rot ticks of the
                      // 100 MHz clock (rc_prio_rotate)
 };
 
-// Wave priority by dispatch order ("the end of a launch").  Every chunk is one
-// lane's serial stream and the chunks are of equal length, so a launch ends with a ramp-down
-// in which the waves dispatched last run with fewer and fewer partners per SIMD.  Issue is
-// arbitrated by priority, then age: at equal priority the oldest wave of a SIMD runs nearly
-// unimpeded and the youngest takes the leftover slots, which stretches the end.  A later
-// workgroup at a higher priority catches up instead.  Scratch control (read at every launch):
-// RC_PRIO_STEP=k sets prio_step = k; RC_PRIO_LAST=n gives the last n workgroups priority 1.
-static inline u32 rc_prio_step(u32 grid) {
-  const char* e = getenv("RC_PRIO_STEP");
-  if (e && *e) return (u32)strtoul(e, nullptr, 10);
-  e = getenv("RC_PRIO_LAST");
-  if (e && *e) {
-    const u32 n = (u32)strtoul(e, nullptr, 10);
-    return n && n < grid ? grid - n : 0u;
+// Wave priority ("the end of a launch").  Every chunk is one lane's serial stream
+// and the chunks are of equal length, so a launch ends with a ramp-down in which the waves
+// dispatched last run with fewer and fewer partners per SIMD.  Issue is arbitrated by priority,
+// then age: at equal priority the oldest wave of a SIMD runs nearly unimpeded and the youngest
+// takes the leftover slots, which stretches the end of the launch.  Two remedies, set per
+// launch by rc_prio_policy from the kernel's residency R (workgroups the chip holds at once):
+//  * static: the workgroups of the last rounds run at a higher priority, so the last-dispatched
+//    waves catch up with the older ones instead of finishing alone;
+//  * rotating (rc_prio_rotate): every 64 symbols a wave sets its priority to ((t >> k) + its
+//    wave slot) mod 4, t = s_memrealtime.  The waves of a SIMD hold distinct slots (HW_ID wave
+//    id), so at any moment they hold different priorities and each takes every priority in
+//    turn: issue goes round-robin at 2^k x 10 ns granularity instead of oldest-first, and waves
+//    that started together finish together (the two waves of one 512-lane workgroup on a SIMD,
+//    whose slots are released together; rounds that divide the grid evenly).
+// Control (read at every launch): RC_PRIO=off; RC_PRIO_LAST=x (the last x rounds at priority
+// 1, x may be fractional), RC_PRIO_RANK=1 (the last three rounds at priorities 1, 2, 3),
+// RC_PRIO_ROT=k (rotation every 2^k ticks, 0 off); unset: the kernel's default.
+struct PrioPolicy {
+  float last_rounds;  // > 0: the last last_rounds x R workgroups at priority 1
+  bool rank;          // the last three rounds at 1, 2, 3
+  u32 rot;            // rotation shift (0: none; kRotAuto: 10 if the grid fits one round, else 12)
+};
+static constexpr u32 kRotAuto = 0xFFu;
+// The kernels' defaults, from same-box stamp runs at 2^20 and 2^17 chunks (DESIGN.md §5,
+// "wave priorities"; profiles/r05/prio_c/):
+//  * encoder (4 waves per SIMD, 16 per SIMD in all at 2^20: four even rounds): rotation every
+//    2^12 ticks (uniform encode -3.1%, Zipf -3.1%, 2^17 -3.8%);
+//  * 256-lane decoders (5 waves per SIMD: 3.2 rounds): the last round at priority 1 (uniform
+//    decode -2.2%; rotation makes their rounds end together and the last 0.2 round alone, +4%);
+//  * 512-lane small-model decoder (two waves of one workgroup per SIMD): rotation, every 2^12
+//    ticks over several rounds (Zipf decode -5.8%), 2^10 when the grid is one round (the 2^17
+//    shard, -4.0%).
+static constexpr PrioPolicy kPrioEncoder{0.0f, false, 12u};
+static constexpr PrioPolicy kPrioDecoder{1.0f, false, 0u};
+static constexpr PrioPolicy kPrioDecoder512{0.0f, false, kRotAuto};
+static inline void rc_prio_policy(ModelArgs& a, PrioPolicy dflt, u32 grid, u32 resident) {
+  a.prio_base = ~0u;
+  a.prio_step = 1u << 31;
+  a.prio_rot = 0;
+  const char* off = getenv("RC_PRIO");
+  if (off && !strcmp(off, "off")) return;
+  PrioPolicy p = dflt;
+  const char* e;
+  if ((e = getenv("RC_PRIO_LAST")) && *e) p = {(float)atof(e), false, 0u};
+  if ((e = getenv("RC_PRIO_RANK")) && *e) p = {0.0f, atoi(e) != 0, 0u};
+  if ((e = getenv("RC_PRIO_ROT")) && *e) p.rot = (u32)strtoul(e, nullptr, 10);
+  if (p.rot == kRotAuto) p.rot = resident && grid > resident ? 12u : 10u;
+  a.prio_rot = p.rot;
+  if (!resident) return;
+  if (p.rank) {
+    a.prio_base = grid > 3 * resident ? grid - 3 * resident : 0u;
+    a.prio_step = resident;
+  } else if (p.last_rounds > 0.0f) {
+    const u32 n = (u32)(p.last_rounds * (float)resident);
+    a.prio_base = n < grid ? grid - n : 0u;
   }
-  return 0u;
-}
-// RC_PRIO_ROT=k: every 64 symbols a wave sets its priority to ((t >> k) + its wave slot) mod 4,
-// t = s_memrealtime.  The waves of a SIMD hold distinct slots (HW_ID wave id), so at any time
-// they hold different priorities and each takes every priority in turn: issue goes round-robin
-// at 2^k x 10 ns granularity instead of oldest-first, and waves that started together stay
-// together (at 4 waves per SIMD and 16 waves per SIMD in all, four even rounds).
-static inline u32 rc_prio_rot() {
-  const char* e = getenv("RC_PRIO_ROT");
-  return e && *e ? (u32)strtoul(e, nullptr, 10) : 0u;
 }
 static __device__ __forceinline__ void rc_prio_rotate(u32 k) {
   if (!k) return;
@@ -135,13 +167,17 @@ static __device__ __forceinline__ void rc_prio_rotate(u32 k) {
   else if (p == 1) __builtin_amdgcn_s_setprio(1);
   else __builtin_amdgcn_s_setprio(0);
 }
-static __device__ __forceinline__ void rc_set_prio(u32 step) {
-  if (!step) return;
-  const u32 p = __builtin_amdgcn_readfirstlane(blockIdx.x / step);
+static __device__ __forceinline__ void rc_set_prio(const ModelArgs& m) {
+  const u32 b = __builtin_amdgcn_readfirstlane(blockIdx.x);
+  if (b < m.prio_base) return;
+  const u32 p = 1u + (b - m.prio_base) / m.prio_step;
   if (p >= 3) __builtin_amdgcn_s_setprio(3);
   else if (p == 2) __builtin_amdgcn_s_setprio(2);
-  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(1);
 }
+// workgroups of `kernel` the current device holds at once with `lds` bytes of dynamic LDS
+// (occupancy x CUs), cached per (device, kernel, lds); 0 when the runtime cannot say (host)
+u32 rc_resident_wgs(const void* kernel, int block, size_t lds);
 
 // Small bucket models (k_decode_static LUT 4: 2048 < total <= 2^16; the pair decoder, LUT 3, is
 // opt-in, RC_DEC_PAIR).  LDS

@@ -80,8 +80,9 @@ def test_ring_fixtures_decode(ctx, ring_fx, monkeypatch, pair, head):
 
 
 def test_ring_fixtures_full_waves(ctx, ring_fx, monkeypatch):
-    """Every fixture in many lanes at once (whole 256-lane workgroups of the bucket decoder, the
-    variant 2^20-chunk launches of this model take), against the oracle's decode."""
+    """Every fixture in many lanes at once (whole workgroups of the bucket decoder, LUT 4: the
+    fixtures' model, total 2^16, has 2^12 buckets and so runs 512-lane workgroups, the variant
+    2^20-chunk launches of this model take), against the oracle's decode."""
     monkeypatch.setenv("RC_DEC_PAIR", "0")
     c = np.array(ring_fx["c"], np.uint32)
     cum = np.array(ring_fx["cum"], np.uint32)
