@@ -21,6 +21,7 @@ of librc_amd.so (include/range_coder.h).  Tensors are torch CUDA(HIP) tensors; P
 used only for device memory and streams.  There is no CPU fallback.
 """
 import ctypes
+import struct
 import math
 
 import numpy as np
@@ -638,10 +639,17 @@ def _canonical_find_index(pmodel):
     """True when decoding may use FreqTable::find_index's binary search (sample_impl.rs:27-45):
     the model does not override find_index (pmodel.rs:12), or says its override has those
     semantics (canonical_find_index = True in the class that defines the override)."""
-    owner = next((k for k in type(pmodel).__mro__ if "find_index" in vars(k)), None)
-    if owner is None or owner is PModel or owner is FreqTable:
-        return True
-    return bool(vars(owner).get("canonical_find_index", False))
+    t = type(pmodel)
+    hit = _CANONICAL.get(t)
+    if hit is None:  # (per class, cached: the MRO scan is ~1 us of every decode call)
+        owner = next((k for k in t.__mro__ if "find_index" in vars(k)), None)
+        hit = (owner is None or owner is PModel or owner is FreqTable or
+               bool(vars(owner).get("canonical_find_index", False)))
+        _CANONICAL[t] = hit
+    return hit
+
+
+_CANONICAL = {}  # PModel class -> whether its find_index keeps FreqTable's semantics
 
 
 def _find_index_rfreq(st, total):
@@ -666,6 +674,9 @@ def _decode_error(st, sig, flags, where):
                 right = mid
         _raise_bad_model(st.lower_bound, st.range, c[left], cum[left], total, where)
     _raise_for_flag(flags, where)
+
+
+_U32_PACK = {}  # alphabet size -> struct.Struct of that many little-endian u32
 
 
 def _table_of(pmodel):
@@ -829,16 +840,21 @@ class Decoder:
 
     def _run(self, st, sig, n):
         """Decode n symbols from state st (updated) under table sig; returns (symbols, flags)."""
-        if self._arrays[0] != sig:
-            self._arrays = (sig, (np.array(sig[0], np.uint32), np.array(sig[1], np.uint32)))
+        na = len(sig[0])
+        if not 1 <= na <= 256 or len(sig[1]) != na:
+            raise RangeCoderError(f"alphabet of {na} symbols (the GPU decoders take 1..256)")
+        if self._arrays[0] != sig:  # the table as packed u32 (struct: ~2 us, numpy ~10-28 us)
+            pk = _U32_PACK.get(na) or _U32_PACK.setdefault(na, struct.Struct(f"<{na}I"))
+            try:
+                self._arrays = (sig, (pk.pack(*sig[0]), pk.pack(*sig[1])))
+            except struct.error as e:
+                raise RangeCoderError(f"table entry outside u32: {e}") from None
         c, cum = self._arrays[1]
-        if not 1 <= len(c) <= 256 or len(cum) != len(c):
-            raise RangeCoderError(f"alphabet of {len(c)} symbols (the GPU decoders take 1..256)")
         out = np.empty(max(n, 1), np.uint8)
         fl = ctypes.c_uint32()
         n0 = st.n
         ctx = self._ctx
-        rc = ctx._lib.rc_stream_decode_host(ctx.handle, _np_ptr(c), _np_ptr(cum), len(c),
+        rc = ctx._lib.rc_stream_decode_host(ctx.handle, c, cum, na,
                                             _u32(sig[2], "total_freq"), ctypes.byref(st),
                                             _np_ptr(self._code), len(self._code), _np_ptr(out),
                                             n, ctypes.byref(fl))

@@ -450,32 +450,42 @@ __global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, co
                    __builtin_amdgcn_readfirstlane((u32)tm);  // wave-uniform (scalar) trip count
   const uint4* tp = live ? reinterpret_cast<const uint4*>(sp + head)
                          : reinterpret_cast<const uint4*>(g_sink);
-  // loads of ENC_TILE_Q 16-B blocks per lane, the next one in flight while the current one is
-  // coded (ENC_TILE_Q 2: 32 registers fewer, for 5 waves per SIMD; scratch builds)
-  constexpr u32 TQ = ENC_TILE_Q;
-  const u64 tstep = live ? TQ : 0;  // uint4s per load
-  const u64 trips = tmin * (4 / TQ);
-  uint4 c[TQ];
-#pragma unroll
-  for (u32 q = 0; q < TQ; ++q) c[q] = make_uint4(0, 0, 0, 0);
+  // 64-symbol tiles, 4 x 16 B per lane, the next tile in flight while the current one is coded
+  // (explicit registers: as arrays the compiler put the tiles in scratch memory, round 5).
+  // ENC_TILE_Q 2 (scratch builds): 32-symbol half tiles, 16 registers fewer.
+  const u64 tstep = live ? ENC_TILE_Q : 0;  // uint4s per load
+  const u64 trips = tmin * (4 / ENC_TILE_Q);
+  uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0;
   if (trips) {
-#pragma unroll
-    for (u32 q = 0; q < TQ; ++q) c[q] = tp[q];
+    c0 = tp[0];
+    c1 = tp[1];
+    if (ENC_TILE_Q == 4) {
+      c2 = tp[2];
+      c3 = tp[3];
+    }
   }
   for (u64 t = 0; t < trips; ++t) {
     rc_prio_rotate(m.prio_rot);
-    uint4 nx[TQ];
-#pragma unroll
-    for (u32 q = 0; q < TQ; ++q) nx[q] = c[q];
+    uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
     if (t + 1 < trips) {
-      const uint4* qp = tp + (t + 1) * tstep;
-#pragma unroll
-      for (u32 q = 0; q < TQ; ++q) nx[q] = qp[q];
+      const uint4* q = tp + (t + 1) * tstep;
+      n0 = q[0];
+      n1 = q[1];
+      if (ENC_TILE_Q == 4) {
+        n2 = q[2];
+        n3 = q[3];
+      }
     }
-#pragma unroll
-    for (u32 q = 0; q < TQ; ++q) enc16<DIV, SM>(e, m, s_tab, c[q], true, lane, wring, wout);
-#pragma unroll
-    for (u32 q = 0; q < TQ; ++q) c[q] = nx[q];
+    enc16<DIV, SM>(e, m, s_tab, c0, true, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c1, true, lane, wring, wout);
+    if (ENC_TILE_Q == 4) {
+      enc16<DIV, SM>(e, m, s_tab, c2, true, lane, wring, wout);
+      enc16<DIV, SM>(e, m, s_tab, c3, true, lane, wring, wout);
+    }
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
   }
   // body, part 2 (ragged waves): the remaining 16-symbol blocks of the tiles, lanes masked
   const u64 nblk = ntile * 4;

@@ -271,6 +271,7 @@ __global__ __launch_bounds__(RWG) void k_stream_decode(
 #define SVC_IDLE_MS 5
 #define SVC_LIFE_MS 2000
 #define SVC_BLOCK (64u << 10)  // request / result block bytes (larger calls take the launch path)
+#define SVC_STOP 0xFFFFFFFFu   // a seq value: leave now (a request number never reaches it)
 enum { SVC_ENCODE = 1, SVC_DECODE = 2 };
 
 struct alignas(64) SvcBox {
@@ -330,11 +331,14 @@ __global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, char* dbox,
   if (lane == 0) sys_store(&box->alive, 2 * epoch + 1);
   const u64 t0 = __builtin_amdgcn_s_memrealtime();
   u64 tl = t0;
+  u32 polls = 0;
   for (;;) {
+    // one load per poll: `stop` is rc_ctx_destroy's (checked every 64 polls), seq == SVC_STOP
+    // is the same request from a caller that holds the mailbox
     const u32 seq = __builtin_amdgcn_readfirstlane(sys_load(&box->seq));
-    const u32 stop = __builtin_amdgcn_readfirstlane(sys_load(&box->stop));
     const u64 now = __builtin_amdgcn_s_memrealtime();
-    if (stop || now - t0 > life_ticks) break;
+    if (seq == SVC_STOP || now - t0 > life_ticks) break;
+    if ((++polls & 63) == 0 && __builtin_amdgcn_readfirstlane(sys_load(&box->stop))) break;
     if (seq == done) {
       if (now - tl > idle_ticks) break;
       __builtin_amdgcn_s_sleep(1);
@@ -389,8 +393,8 @@ __global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, char* dbox,
     char* const hblk = hbox + sizeof(SvcBox);
     svc_copy(hblk, dblk, 0, head_b, lane);
     svc_copy(hblk, dblk, t_off, t_b, lane);
-    __threadfence_system();
-    __syncthreads();
+    // (the release below waits for every store of this one-wave workgroup, all lanes: vmcnt
+    // counts per wave, so no separate system fence)
     if (lane == 0) sys_store(&box->ack, seq);
     done = seq;
     tl = __builtin_amdgcn_s_memrealtime();
@@ -549,7 +553,8 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, Fill fill, rc_status* err) {
   }
   SvcBox* b = sv->box;
   fill((char*)(b + 1), b);
-  const u32 s = ++sv->seq;
+  if (++sv->seq == SVC_STOP) sv->seq = 1;  // (SVC_STOP is the stop request, never a number)
+  const u32 s = sv->seq;
   __atomic_store_n(&b->seq, s, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   for (u32 spin = 0;; ++spin) {

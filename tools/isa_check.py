@@ -83,7 +83,20 @@ def _descriptors(co_path):
             sa, so = secs[int(p[6])]
             rsrc1 = struct.unpack_from("<I", data, so + addr - sa + 48)[0]
             alloc[p[7][:-3]] = ((rsrc1 & 63) + 1) * 8
+            # (kernel descriptor offset 4: private_segment_fixed_size, scratch bytes per lane)
+            SCRATCH[p[7][:-3]] = struct.unpack_from("<I", data, so + addr - sa + 4)[0]
     return alloc
+
+
+SCRATCH = {}  # kernel -> scratch bytes per lane, filled by check_code_object
+
+
+def scratch_sizes(lib):
+    """{kernel: scratch (private segment) bytes per lane} of every gfx950 kernel in lib."""
+    SCRATCH.clear()
+    for co in code_objects(lib):
+        check_code_object(co)
+    return dict(SCRATCH)
 
 
 def _vregs(operand):
@@ -139,6 +152,7 @@ def check_code_object(blob):
 
 
 def check_library(lib):
+    SCRATCH.clear()
     out = {}
     for blob in code_objects(lib):
         out.update(check_code_object(blob))
