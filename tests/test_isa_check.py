@@ -43,3 +43,15 @@ def test_shipped_library_passes():
     res = isa_check.check_library(LIB)
     assert len(res) >= 30
     assert not {k: v for k, v in res.items() if v[2]}
+
+
+def test_shipped_coders_use_no_scratch():
+    """The static coders keep their state and tiles in registers: build() refuses a library in
+    which one uses scratch memory (round 5: an array form of the encoder's tile loop put the
+    tiles in scratch and halved its rate)."""
+    if not os.path.exists(LIB):
+        pytest.skip("library not built")
+    sizes = isa_check.scratch_sizes(LIB)
+    coders = {k: v for k, v in sizes.items() if "k_encode_static" in k or "k_decode_static" in k}
+    assert coders, "no coder kernels found"
+    assert not {k: v for k, v in coders.items() if v}, coders
