@@ -2,7 +2,7 @@
 # What binds the static kernels: per configuration (uniform: direct-table
 # decoder; zipf: bucket decoder) one kernel-trace pass (durations, VGPR counts) and two SQ counter
 # passes with the GRBM clock counters, over one launch of each kernel at 2^20 x 64 KiB; "shard":
-# the configs[4] N = 8 shard (2^17 Zipf chunks: the pair decoder, 2 waves per SIMD).
+# the configs[4] N = 8 shard (2^17 Zipf chunks: the LUT 4 bucket decoder in 512-lane workgroups).
 # Usage on the GPU box:  [CONFIGS="shard"] bash tools/pmc_bound.sh TAG   -> gpurun_out/bound_<TAG>/
 # then locally: python3 tools/pmc_bound.py gpurun_out/bound_<TAG>
 set -euo pipefail
