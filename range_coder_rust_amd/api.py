@@ -815,10 +815,14 @@ class Decoder:
     sample_impl.rs:113-120) only bounds the decode-ahead."""
 
     MAX_BLOCK = 1 << 20
+    SMALL = 64  # calls of up to this many symbols decode into a reused buffer
 
     def __init__(self, code, n_symbols=None, ctx=None):
         self._ctx = ctx or default_context()
         self._code = np.frombuffer(bytes(code), dtype=np.uint8)
+        self._code_ptr = _np_ptr(self._code)  # (the array lives as long as the decoder)
+        self._small = ctypes.create_string_buffer(self.SMALL)  # output of the short calls
+        self._fl = ctypes.c_uint32()
         self._limit = None if n_symbols is None else int(n_symbols)
         self._arrays = (None, None)  # table signature -> (c, cum) uint32 arrays
         st = N.StreamState.fresh()
@@ -850,17 +854,19 @@ class Decoder:
             except struct.error as e:
                 raise RangeCoderError(f"table entry outside u32: {e}") from None
         c, cum = self._arrays[1]
-        out = np.empty(max(n, 1), np.uint8)
-        fl = ctypes.c_uint32()
+        small = n <= self.SMALL
+        out = self._small if small else np.empty(n, np.uint8)
+        fl = self._fl
         n0 = st.n
         ctx = self._ctx
         rc = ctx._lib.rc_stream_decode_host(ctx.handle, c, cum, na,
                                             _u32(sig[2], "total_freq"), ctypes.byref(st),
-                                            _np_ptr(self._code), len(self._code), _np_ptr(out),
-                                            n, ctypes.byref(fl))
+                                            self._code_ptr, len(self._code),
+                                            out if small else _np_ptr(out), n, ctypes.byref(fl))
         if rc not in (N.RC_OK, N.RC_E_CHUNK):
             N.check(rc, "rc_stream_decode_host")
-        return out[: st.n - n0], fl.value
+        got = st.n - n0
+        return (out.raw[:got] if small else out[:got]), fl.value
 
     @staticmethod
     def _copy(st):

@@ -127,6 +127,34 @@ void* rc_pinned_scratch_(size_t bytes) {
   return t_pinned.p;
 }
 
+// range_par_total's constants for `total` (DIV_POW2's shift, DIV_MAGIC's reciprocal and the
+// small models' f64 1/total rounded up)
+static void div_constants(ModelArgs& a, u32 total) {
+  const bool pow2 = (total & (total - 1)) == 0;
+  a.total = total;
+  a.lg = pow2 ? (u32)__builtin_ctz(total) : 0u;
+  a.magic = ~0ull / (u64)total;
+  a.inv_up = 1.0 / (double)total;  // rounded up: inv_up * total >= 1 exactly
+  if (std::fma(a.inv_up, (double)total, -1.0) < 0.0) a.inv_up = std::nextafter(a.inv_up, 2.0);
+}
+
+// range / total through the static coders' three range_par_total forms (rc_static.h), under
+// the decoders' rounding mode (f32 toward zero, rc_decode.inc): out[3i] the small-model f64
+// form, out[3i + 1] the 64 x 64 magic product, out[3i + 2] the power-of-two shift.  For
+// rc_test_range_par_total_ (tests/test_gpu_div.py).
+__global__ __launch_bounds__(64) void k_test_range_par_total(const u64* __restrict__ ranges,
+                                                             const ModelArgs* __restrict__ ms,
+                                                             u32 n, u64* __restrict__ out) {
+  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 2), 3");
+  const u32 i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const ModelArgs m = ms[i];
+  const u64 r = ranges[i];
+  out[3 * i] = range_par_total<DIV_MAGIC, 1>(r, m);
+  out[3 * i + 1] = range_par_total<DIV_MAGIC, 0>(r, m);
+  out[3 * i + 2] = range_par_total<DIV_POW2, 0>(r, m);
+}
+
 extern "C" {
 
 const char* rc_last_error(void) { return g_last_error; }
@@ -262,11 +290,8 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
   a.n = n_symbols;
   a.total = total_freq;
   a.ftotal = (float)total_freq;
+  div_constants(a, total_freq);
   const bool pow2 = (total_freq & (total_freq - 1)) == 0;
-  a.lg = pow2 ? (u32)__builtin_ctz(total_freq) : 0u;
-  a.magic = ~0ull / (u64)total_freq;
-  a.inv_up = 1.0 / (double)total_freq;  // rounded up: inv_up * total >= 1 exactly
-  if (std::fma(a.inv_up, (double)total_freq, -1.0) < 0.0) a.inv_up = std::nextafter(a.inv_up, 2.0);
   // bucket table of 2^bits buckets: s0 = symbol containing the bucket's first frequency, s1 =
   // the next symbol with c > 0 starting inside the bucket, split = its offset (0xFFFF: none);
   // padded to a power of two (the kernel masks the bucket index) with the last bucket, so
@@ -532,6 +557,37 @@ rc_status rc_synth_fill(rc_ctx* ctx, uint64_t seed, const uint8_t* inv_cdf_host,
   // the pinned staging is reused by this thread's next call: wait for the copy
   if (st == RC_OK && (e = hipStreamSynchronize(ctx->cur)) != hipSuccess)
     return device_error(e, "rc_synth_fill sync");
+  return st;
+}
+
+// Internal test hook (not in include/range_coder.h): range / total for n (range, total) pairs
+// through k_test_range_par_total; out: 3 n results (host memory).  Synchronous.
+rc_status rc_test_range_par_total_(rc_ctx* ctx, const uint64_t* ranges, const uint32_t* totals,
+                                   uint32_t n, uint64_t* out) {
+  if (!ctx || !ranges || !totals || !out || n == 0 || n > (1u << 20)) return RC_E_ARG;
+  std::vector<ModelArgs> ms(n);
+  for (u32 i = 0; i < n; ++i) {
+    if (totals[i] == 0) return RC_E_BAD_MODEL;
+    memset(&ms[i], 0, sizeof(ModelArgs));
+    div_constants(ms[i], totals[i]);
+  }
+  DeviceGuard g(ctx->device);
+  char* d = nullptr;
+  const size_t b_r = 8ull * n, b_m = sizeof(ModelArgs) * n, b_o = 24ull * n;
+  if (hipMalloc((void**)&d, b_r + b_m + b_o) != hipSuccess) return RC_E_DEVICE;
+  rc_status st = RC_OK;
+  if (hipMemcpy(d, ranges, b_r, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d + b_r, ms.data(), b_m, hipMemcpyHostToDevice) != hipSuccess) {
+    st = RC_E_DEVICE;
+  } else {
+    hipLaunchKernelGGL(k_test_range_par_total, dim3((n + 63) / 64), dim3(64), 0, ctx->cur,
+                       (const u64*)d, (const ModelArgs*)(d + b_r), n, (u64*)(d + b_r + b_m));
+    st = launch_status();
+    if (st == RC_OK && (hipStreamSynchronize(ctx->cur) != hipSuccess ||
+                        hipMemcpy(out, d + b_r + b_m, b_o, hipMemcpyDeviceToHost) != hipSuccess))
+      st = RC_E_DEVICE;
+  }
+  (void)hipFree(d);
   return st;
 }
 

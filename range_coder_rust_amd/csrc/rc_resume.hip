@@ -18,6 +18,7 @@
 //   decoder needs a byte past the end -> RC_F_TRUNCATED (pop_front().unwrap(), decoder.rs:33)
 // u64 products wrap (release-build semantics of the reference).
 #include "rc_common.h"
+#include "rc_udiv.h"
 
 #include <stddef.h>
 #include <string.h>
@@ -41,14 +42,10 @@ struct Narrow {
   u32 err;
 };
 
-static __device__ __forceinline__ Narrow narrow(u64 low, u64 range, u32 c, u32 cum, u32 total,
-                                                u32 zero_flag) {
+// (r = range_par_total, range_coder.rs:38-40)
+static __device__ __forceinline__ Narrow narrow_r(u64 low, u64 range, u64 r, u32 c, u32 cum,
+                                                  u32 zero_flag) {
   Narrow o{low, range, 0u};
-  if (total == 0) {  // range_par_total (range_coder.rs:38-40) divides by zero
-    o.err = RC_F_BAD_MODEL;
-    return o;
-  }
-  const u64 r = range / (u64)total;
   const u64 nr = r * (u64)c;     // range_coder.rs:65
   const u64 add = r * (u64)cum;  // :68
   const u64 nl = low + add;
@@ -58,6 +55,11 @@ static __device__ __forceinline__ Narrow narrow(u64 low, u64 range, u32 c, u32 c
   o.low = nl;
   o.range = nr;
   return o;
+}
+static __device__ __forceinline__ Narrow narrow(u64 low, u64 range, u32 c, u32 cum, u32 total,
+                                                u32 zero_flag) {
+  if (total == 0) return Narrow{low, range, RC_F_BAD_MODEL};  // range_par_total divides by 0
+  return narrow_r(low, range, rc_udiv64(range, total), c, cum, zero_flag);
 }
 
 // bytes the two renormalisation loops settle from (low, range), without applying them
@@ -77,7 +79,16 @@ static __device__ __forceinline__ u32 settle_count(u64 low, u64 range) {
   return k;
 }
 
+// byte store into the body's block: global memory (the launch path) or LDS (the service; the
+// pointer is generic, derived from the LDS block, and the compiler infers the address space)
+template <bool kLds>
+static __device__ __forceinline__ void bstore(uint8_t* p, u32 v) {
+  if constexpr (kLds) *p = (uint8_t)v;
+  else gstore8(p, v);
+}
+
 // Encoder::encode x n (+ finish) for stream k (the body of k_stream_encode and of the service)
+template <bool kLds>
 static __device__ void stream_encode_one(
     u32 k, rc_stream_state* __restrict__ st, const u32* __restrict__ trip,
     const u64* __restrict__ sym_off, uint8_t* __restrict__ out, const u64* __restrict__ out_off,
@@ -114,24 +125,24 @@ static __device__ void stream_encode_one(
     range = q.range;
     u32 nb = 0;
     while (((low ^ (low + range)) >> 56) == 0) {  // no_carry_expansion (:110-116)
-      gstore8(o + w++, (u32)(low >> 56));       // left_shift (:95-100)
+      bstore<kLds>(o + w++, (u32)(low >> 56));  // left_shift (:95-100)
       low <<= 8;
       range <<= 8;
       ++nb;
     }
     while (range < TOP16) {  // range_reduction_expansion (:126-135)
       range = ~low & (TOP16 - 1);
-      gstore8(o + w++, (u32)(low >> 56));
+      bstore<kLds>(o + w++, (u32)(low >> 56));
       low <<= 8;
       range <<= 8;
       ++nb;
     }
-    if (nbytes) gstore8(nbytes + s0 + i, nb);  // encode()'s return value (encoder.rs:34-36)
+    if (nbytes) bstore<kLds>(nbytes + s0 + i, nb);  // encode()'s return value (encoder.rs:34-36)
     S.n += 1;
   }
   if (finish && !S.flags) {  // Encoder::finish: 8 x left_shift (encoder.rs:40-46)
     for (int j = 0; j < 8; ++j) {
-      gstore8(o + w++, (u32)(low >> 56));
+      bstore<kLds>(o + w++, (u32)(low >> 56));
       low <<= 8;
       range <<= 8;
     }
@@ -155,11 +166,12 @@ __global__ __launch_bounds__(RWG) void k_stream_encode(
   const u32 k = blockIdx.x * RWG + threadIdx.x;
   if (k >= n_streams) return;
   RC_VGPR_FLOOR_48();
-  stream_encode_one(k, st, trip, sym_off, out, out_off, out_len, nbytes, finish, flags);
+  stream_encode_one<false>(k, st, trip, sym_off, out, out_off, out_len, nbytes, finish, flags);
 }
 
 // Decoder::decode x n for stream k against the table in LDS (the body of k_stream_decode and of
 // the service)
+template <bool kLds>
 static __device__ void stream_decode_one(
     u32 k, const u32* s_c, const u32* s_cum, u32 n_alpha, u32 total,
     rc_stream_state* __restrict__ st, const uint8_t* __restrict__ code,
@@ -192,15 +204,37 @@ static __device__ void stream_decode_one(
       S.flags = RC_F_BAD_MODEL;
       break;
     }
-    // FreqTable::find_index (sample_impl.rs:27-45): rfreq, then the binary search over cum
-    const u64 rfreq = (data - low) / (range / (u64)total);
+    // FreqTable::find_index (sample_impl.rs:27-45): rfreq, then the binary search over cum.
+    // (r == 0 divides by zero there; param_update below then flags the step, r * c == 0.)
+    const u64 r = rc_udiv64(range, total);
+    const u64 rfreq = r ? rc_udiv64(data - low, r) : 0;
     u32 left = 0, right = n_alpha - 1;
-    while (left < right) {
-      const u32 mid = (left + right) >> 1;
-      if ((u64)s_cum[mid + 1] <= rfreq) left = mid + 1;
-      else right = mid;
+    if constexpr (kLds) {
+      // the service: the whole wave runs this body on the same values, so every comparison
+      // the search could make (cum[j + 1] <= rfreq, j < n_alpha - 1) is taken at once, four
+      // per lane, into a 256-bit mask; the search then walks the mask, step for step the same
+      // bisection, without an LDS round trip per step
+      const u32 lane = threadIdx.x;
+      u64 m[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const u32 j = lane + 64 * h;
+        m[h] = __ballot(j + 1 < n_alpha && (u64)s_cum[j + 1] <= rfreq);
+      }
+      while (left < right) {
+        const u32 mid = (left + right) >> 1;
+        const u64 w = mid < 64 ? m[0] : mid < 128 ? m[1] : mid < 192 ? m[2] : m[3];
+        if ((w >> (mid & 63)) & 1) left = mid + 1;
+        else right = mid;
+      }
+    } else {
+      while (left < right) {
+        const u32 mid = (left + right) >> 1;
+        if ((u64)s_cum[mid + 1] <= rfreq) left = mid + 1;
+        else right = mid;
+      }
     }
-    const Narrow q = narrow(low, range, s_c[left], s_cum[left], total, RC_F_CORRUPT);
+    const Narrow q = narrow_r(low, range, r, s_c[left], s_cum[left], RC_F_CORRUPT);
     if (q.err) {
       S.flags = q.err;
       break;
@@ -222,7 +256,7 @@ static __device__ void stream_decode_one(
       range <<= 8;
     }
     for (u32 j = 0; j < nb; ++j) data = (data << 8) | cp[pos++];
-    gstore8(syms + s0 + i, left);
+    bstore<kLds>(syms + s0 + i, left);
     S.n += 1;
   }
   S.lower_bound = low;
@@ -248,8 +282,8 @@ __global__ __launch_bounds__(RWG) void k_stream_decode(
   const u32 k = blockIdx.x * RWG + threadIdx.x;
   if (k >= n_streams) return;
   RC_VGPR_FLOOR_64();
-  stream_decode_one(k, s_c, s_cum, n_alpha, total, st, code, code_off, code_len, syms, sym_off,
-                    flags);
+  stream_decode_one<false>(k, s_c, s_cum, n_alpha, total, st, code, code_off, code_len, syms,
+                           sym_off, flags);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -261,12 +295,13 @@ __global__ __launch_bounds__(RWG) void k_stream_decode(
 //
 // The mailbox is pinned, coherent, device-mapped host memory.  The host writes the request
 // block (the same layout the launch path copies to the device) and then `seq` (release); the
-// wave polls `seq` (system-scope acquire), copies the block into device scratch with all 64
-// lanes, runs the same per-stream body as the launch path on lane 0, copies the result ranges
-// back into the mailbox and sets `ack` (release).  It leaves on `stop`, after SVC_IDLE_MS
-// without a request, or after SVC_LIFE_MS in all, so it never outlives its caller for long: a
-// later call starts a new one (an epoch: `alive` is 2 epoch + 1 while epoch's wave runs and
-// 2 epoch + 2 once it left).  Every exit condition is checked on every poll.
+// wave polls `seq` (system-scope acquire), reads the header and block into LDS with all 64
+// lanes, runs the same per-stream body as the launch path on lane 0 against the block in LDS
+// (so the body's loads and stores cost LDS latency, not device-memory round trips), writes the
+// result ranges back into the mailbox and sets `ack` (release).  It leaves on `stop`, after
+// SVC_IDLE_MS without a request, or after SVC_LIFE_MS in all, so it never outlives its caller
+// for long: a later call starts a new one (an epoch: `alive` is 2 epoch + 1 while epoch's wave
+// runs and 2 epoch + 2 once it left).  Every exit condition is checked on every poll.
 // ------------------------------------------------------------------------------------------
 #define SVC_IDLE_MS 5
 #define SVC_LIFE_MS 2000
@@ -287,26 +322,30 @@ struct alignas(64) SvcBox {
   u32 p4[4];
 };
 static_assert(sizeof(SvcBox) == 384, "mailbox header layout");
+// header + block in LDS (one workgroup may hold up to 160 KiB on gfx950)
+static_assert(sizeof(SvcBox) + SVC_BLOCK <= 96u << 10, "service LDS block");
 
 static __device__ __forceinline__ u32 sys_load(const u32* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-// header fields of the current request (vector loads at system scope, after the acquire of seq)
-static __device__ __forceinline__ u32 hdr32(const u32* p) {
-  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-}
-static __device__ __forceinline__ u64 hdr64(const u64* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 static __device__ __forceinline__ void sys_store(u32* p, u32 v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// copy [off, off + bytes) (16-B multiples) from src to dst with the wave's 64 lanes
+// copy [off, off + bytes) (16-B multiples) from src to dst with the wave's 64 lanes, eight
+// 16-B loads in flight per lane before the first store
 static __device__ __forceinline__ void svc_copy(char* dst, const char* src, u64 off, u64 bytes,
                                                 u32 lane) {
-  for (u64 i = off + 16 * lane; i < off + bytes; i += 16 * RWG)
-    *(u32x4*)(dst + i) = *(const volatile u32x4*)(src + i);
+  const u64 end = off + bytes;
+  u64 i = off + 16 * lane;
+  for (; i + 7 * 16 * RWG < end; i += 8 * 16 * RWG) {
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = *(const u32x4*)(src + i + j * 16 * RWG);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *(u32x4*)(dst + i + j * 16 * RWG) = v[j];
+  }
+  for (; i < end; i += 16 * RWG) *(u32x4*)(dst + i) = *(const u32x4*)(src + i);
 }
 
 #define SVC_BURST 4096u  // bytes of the mailbox read in one burst (header + the block's start)
@@ -321,12 +360,12 @@ static __device__ __forceinline__ u64 burst64(const u32x4* v, u32 off) {
   return ((u64)burst32(v, off + 4) << 32) | burst32(v, off);
 }
 
-__global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, char* dbox, u32 epoch,
-                                                        u64 idle_ticks, u64 life_ticks) {
-  __shared__ u32 s_c[256], s_cum[256];
+__global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, u32 epoch, u64 idle_ticks,
+                                                        u64 life_ticks) {
+  __shared__ __attribute__((aligned(16))) char s_box[sizeof(SvcBox) + SVC_BLOCK];
   const u32 lane = threadIdx.x;
   char* const hbox = (char*)box;
-  char* const dblk = dbox + sizeof(SvcBox);
+  char* const sblk = s_box + sizeof(SvcBox);
   u32 done = __builtin_amdgcn_readfirstlane(sys_load(&box->ack));
   if (lane == 0) sys_store(&box->alive, 2 * epoch + 1);
   const u64 t0 = __builtin_amdgcn_s_memrealtime();
@@ -360,39 +399,33 @@ __global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, char* dbox,
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = burst64(v, offsetof(SvcBox, o) + 8 * j);
 #pragma unroll
-    for (u32 j = 0; j < SVC_BURST / 1024; ++j) *(u32x4*)(dbox + 16 * (lane + 64 * j)) = v[j];
+    for (u32 j = 0; j < SVC_BURST / 1024; ++j) *(u32x4*)(s_box + 16 * (lane + 64 * j)) = v[j];
     if (sizeof(SvcBox) + in_b > SVC_BURST)
-      svc_copy(dbox, hbox, SVC_BURST, sizeof(SvcBox) + in_b - SVC_BURST, lane);
-    __threadfence_block();
+      svc_copy(s_box, hbox, SVC_BURST, sizeof(SvcBox) + in_b - SVC_BURST, lane);
     __syncthreads();
     if (op == SVC_DECODE) {
       const u32 na = burst32(v, offsetof(SvcBox, n_alpha)), tot = burst32(v, offsetof(SvcBox, total));
-      for (u32 j = lane; j < na; j += RWG) {
-        s_c[j] = ((const u32*)(dblk + o[2]))[j];
-        s_cum[j] = ((const u32*)(dblk + o[3]))[j];
-      }
-      __syncthreads();
       // block: state | offsets (code_off, code_len, sym_off[0..1]) | flags | c | cum | window | syms
-      if (lane == 0)
-        stream_decode_one(0, s_c, s_cum, na, tot, (rc_stream_state*)dblk,
-                          (const uint8_t*)(dblk + o[4]), (const u64*)(dblk + o[0]),
-                          (const u64*)(dblk + o[0] + 8), (uint8_t*)(dblk + o[5]),
-                          (const u64*)(dblk + o[0] + 16), (u32*)(dblk + o[1]));
+      // (all lanes: the search is wave-wide; every lane computes and stores the same values)
+      stream_decode_one<true>(0, (const u32*)(sblk + o[2]), (const u32*)(sblk + o[3]), na, tot,
+                                (rc_stream_state*)sblk, (const uint8_t*)(sblk + o[4]),
+                                (const u64*)(sblk + o[0]), (const u64*)(sblk + o[0] + 8),
+                                (uint8_t*)(sblk + o[5]), (const u64*)(sblk + o[0] + 16),
+                                (u32*)(sblk + o[1]));
     } else if (op == SVC_ENCODE) {
       const u32 fin = burst32(v, offsetof(SvcBox, finish));
       // block: state | offsets (sym_off[0..1], out_off[0..1]) | out_len | flags | triples | nb | out
       if (lane == 0)
-        stream_encode_one(0, (rc_stream_state*)dblk, (const u32*)(dblk + o[3]),
-                          (const u64*)(dblk + o[0]), (uint8_t*)(dblk + o[5]),
-                          (const u64*)(dblk + o[0] + 16), (u64*)(dblk + o[1]),
-                          o[6] ? (uint8_t*)(dblk + o[4]) : (uint8_t*)nullptr, fin,
-                          (u32*)(dblk + o[2]));
+        stream_encode_one<true>(0, (rc_stream_state*)sblk, (const u32*)(sblk + o[3]),
+                                (const u64*)(sblk + o[0]), (uint8_t*)(sblk + o[5]),
+                                (const u64*)(sblk + o[0] + 16), (u64*)(sblk + o[1]),
+                                o[6] ? (uint8_t*)(sblk + o[4]) : (uint8_t*)nullptr, fin,
+                                (u32*)(sblk + o[2]));
     }
-    __threadfence();
     __syncthreads();
     char* const hblk = hbox + sizeof(SvcBox);
-    svc_copy(hblk, dblk, 0, head_b, lane);
-    svc_copy(hblk, dblk, t_off, t_b, lane);
+    svc_copy(hblk, sblk, 0, head_b, lane);
+    svc_copy(hblk, sblk, t_off, t_b, lane);
     // (the release below waits for every store of this one-wave workgroup, all lanes: vmcnt
     // counts per wave, so no separate system fence)
     if (lane == 0) sys_store(&box->ack, seq);
@@ -478,7 +511,6 @@ struct Svc {
   std::mutex mu;
   SvcBox* box = nullptr;  // host address of the mailbox (header, then the block)
   SvcBox* dbox_host = nullptr;  // device address of the mailbox (mapped host memory)
-  char* dbox = nullptr;         // device scratch mirroring the mailbox (header + block)
   hipStream_t stream = nullptr;
   u32 epoch = 0, seq = 0;
   bool launched = false, dead = false, broken = false;
@@ -517,10 +549,8 @@ void svc_teardown(Svc* sv) {
   }
   if (sv->stream) (void)hipStreamDestroy(sv->stream);
   if (sv->box) (void)hipHostFree(sv->box);
-  if (sv->dbox) (void)hipFree(sv->dbox);
   sv->stream = nullptr;
   sv->box = nullptr;
-  sv->dbox = nullptr;
   sv->dbox_host = nullptr;
   sv->launched = false;
 }
@@ -543,7 +573,6 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, Fill fill, rc_status* err) {
     sv->box = (SvcBox*)hb;
     void* dp = nullptr;
     if (hipHostGetDevicePointer(&dp, hb, 0) != hipSuccess ||
-        hipMalloc((void**)&sv->dbox, sizeof(SvcBox) + SVC_BLOCK) != hipSuccess ||
         hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess) {
       svc_teardown(sv);
       sv->broken = true;
@@ -563,7 +592,7 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, Fill fill, rc_status* err) {
     if (!sv->launched || __atomic_load_n(&b->alive, __ATOMIC_ACQUIRE) == 2 * sv->epoch + 2) {
       ++sv->epoch;
       hipLaunchKernelGGL(k_stream_service, dim3(1), dim3(RWG), 0, sv->stream, sv->dbox_host,
-                         sv->dbox, sv->epoch, (u64)SVC_IDLE_MS * 100000ull,
+                         sv->epoch, (u64)SVC_IDLE_MS * 100000ull,
                          (u64)SVC_LIFE_MS * 100000ull);
       if (hipGetLastError() != hipSuccess) {
         sv->broken = true;

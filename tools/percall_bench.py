@@ -112,6 +112,20 @@ def main():
         res["_code"] = enc.finish()
     res["adaptive_encode_us"] = us_per(run_aenc, n_adapt) - res["adaptive_update_us"]
     acode = res.pop("_code")
+
+    # encode() with its return value read at every call (encoder.rs:34-36): a flush per symbol
+    m = Adaptive()
+    enc = rc.Encoder()
+    cnt = []
+
+    def run_aenc_count():
+        for i, s in enumerate(asy):
+            cnt.append(int(enc.encode(m, s)))
+            m.update(s, i)
+        res["_code"] = enc.finish()
+    res["adaptive_encode_count_us"] = (us_per(run_aenc_count, n_adapt)
+                                       - res["adaptive_update_us"])
+    assert res.pop("_code") == acode and sum(cnt) + 8 == len(acode)
     m = Adaptive()
     dec = rc.Decoder(acode)
     got = []
