@@ -702,9 +702,11 @@ class Encoder:
     subclasses at the call that flushes them; the encoder is then unusable, as after a panic."""
 
     FLUSH_AT = 1 << 20
+    SMALL = 64  # flushes of up to this many symbols use reused ctypes buffers
 
     def __init__(self, ctx=None):
         self._ctx = ctx
+        self._bufs = None          # (triples, output, counts) ctypes buffers of the small flushes
         self._state = N.StreamState.fresh()
         self._code = bytearray()
         self._trip = []            # staged (c, cum, total), flat
@@ -765,21 +767,35 @@ class Encoder:
         if n == 0 and not finish:
             return
         ctx = self._ctx or default_context()
-        trip = np.array(self._trip, dtype=np.uint32)
         cap = N.stream_max_bytes(n, finish)
-        out = np.empty(max(cap, 1), np.uint8)
-        nb = np.empty(max(n, 1), np.uint8)
+        small = n <= self.SMALL
+        if small:  # (numpy arrays and their .ctypes cost ~1 us each per call)
+            if self._bufs is None:
+                self._bufs = ((ctypes.c_uint32 * (3 * self.SMALL))(),
+                              ctypes.create_string_buffer(N.stream_max_bytes(self.SMALL, True)),
+                              ctypes.create_string_buffer(self.SMALL))
+            tb, out, nb = self._bufs
+            tb[: 3 * n] = self._trip
+            args = (tb, out, nb)
+        else:
+            out = np.empty(max(cap, 1), np.uint8)
+            nb = np.empty(max(n, 1), np.uint8)
+            args = (_np_ptr(np.array(self._trip, dtype=np.uint32)), _np_ptr(out), _np_ptr(nb))
         out_len = ctypes.c_uint64()
         fl = ctypes.c_uint32()
         n0 = self._state.n
-        rc = ctx._lib.rc_stream_encode_host(ctx.handle, ctypes.byref(self._state), _np_ptr(trip),
-                                            n, _np_ptr(out), cap, ctypes.byref(out_len),
-                                            _np_ptr(nb), 1 if finish else 0, ctypes.byref(fl))
+        rc = ctx._lib.rc_stream_encode_host(ctx.handle, ctypes.byref(self._state), args[0], n,
+                                            args[1], cap, ctypes.byref(out_len), args[2],
+                                            1 if finish else 0, ctypes.byref(fl))
         if rc not in (N.RC_OK, N.RC_E_CHUNK):
             N.check(rc, "rc_stream_encode_host")
-        self._code += out[: out_len.value].tobytes()
         done = self._state.n - n0
-        self._counts += nb[:done].tobytes()
+        if small:
+            self._code += out.raw[: out_len.value]
+            self._counts += nb.raw[:done]
+        else:
+            self._code += out[: out_len.value].tobytes()
+            self._counts += nb[:done].tobytes()
         failed = self._trip[3 * done: 3 * done + 3]
         self._staged0 += n
         self._trip = []
