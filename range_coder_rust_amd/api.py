@@ -780,7 +780,8 @@ class Encoder:
         else:
             out = np.empty(max(cap, 1), np.uint8)
             nb = np.empty(max(n, 1), np.uint8)
-            args = (_np_ptr(np.array(self._trip, dtype=np.uint32)), _np_ptr(out), _np_ptr(nb))
+            trip = np.array(self._trip, dtype=np.uint32)  # (held: _np_ptr keeps no reference)
+            args = (_np_ptr(trip), _np_ptr(out), _np_ptr(nb))
         out_len = ctypes.c_uint64()
         fl = ctypes.c_uint32()
         n0 = self._state.n

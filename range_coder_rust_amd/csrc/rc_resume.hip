@@ -319,7 +319,8 @@ struct alignas(64) SvcBox {
   u64 head_bytes;             // result head [0, head_bytes) copied back (multiple of 16)
   u64 tail_off, tail_bytes;   // result tail [tail_off, + tail_bytes) copied back (multiples of 16)
   u64 o[8];                   // byte offsets of the body's arguments inside the block
-  u32 p4[4];
+  u32 probe[4];  // wave -> host: 10-ns ticks from seeing seq to: block in LDS, body done,
+                 // results written (rc_svc_probe_)
 };
 static_assert(sizeof(SvcBox) == 384, "mailbox header layout");
 // header + block in LDS (one workgroup may hold up to 160 KiB on gfx950)
@@ -383,6 +384,7 @@ __global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, u32 epoch, 
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
+    const u64 td = now;
     // The request in one burst: the first 4 KiB of the mailbox (header and block), every load
     // in flight before the first is used, so a one-symbol call costs one PCIe round trip; the
     // header fields come out of the lanes' registers.  (Plain loads: the acquire of seq orders
@@ -403,6 +405,7 @@ __global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, u32 epoch, 
     if (sizeof(SvcBox) + in_b > SVC_BURST)
       svc_copy(s_box, hbox, SVC_BURST, sizeof(SvcBox) + in_b - SVC_BURST, lane);
     __syncthreads();
+    const u64 t1 = __builtin_amdgcn_s_memrealtime();
     if (op == SVC_DECODE) {
       const u32 na = burst32(v, offsetof(SvcBox, n_alpha)), tot = burst32(v, offsetof(SvcBox, total));
       // block: state | offsets (code_off, code_len, sym_off[0..1]) | flags | c | cum | window | syms
@@ -423,9 +426,15 @@ __global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, u32 epoch, 
                                 (u32*)(sblk + o[2]));
     }
     __syncthreads();
+    const u64 t2 = __builtin_amdgcn_s_memrealtime();
     char* const hblk = hbox + sizeof(SvcBox);
     svc_copy(hblk, sblk, 0, head_b, lane);
     svc_copy(hblk, sblk, t_off, t_b, lane);
+    if (lane == 0) {
+      const u64 t3 = __builtin_amdgcn_s_memrealtime();
+      u32x4 pr = {(u32)(t1 - td), (u32)(t2 - td), (u32)(t3 - td), 0u};
+      *(u32x4*)box->probe = pr;
+    }
     // (the release below waits for every store of this one-wave workgroup, all lanes: vmcnt
     // counts per wave, so no separate system fence)
     if (lane == 0) sys_store(&box->ack, seq);
@@ -514,6 +523,7 @@ struct Svc {
   hipStream_t stream = nullptr;
   u32 epoch = 0, seq = 0;
   bool launched = false, dead = false, broken = false;
+  u64 probe[5] = {0, 0, 0, 0, 0};  // calls, the wave's three intervals, the host's wait (ns)
 };
 std::mutex g_svc_mu;
 std::unordered_map<const rc_ctx*, std::shared_ptr<Svc>> g_svcs;
@@ -587,7 +597,13 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, Fill fill, rc_status* err) {
   __atomic_store_n(&b->seq, s, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   for (u32 spin = 0;; ++spin) {
-    if (__atomic_load_n(&b->ack, __ATOMIC_ACQUIRE) == s) return true;
+    if (__atomic_load_n(&b->ack, __ATOMIC_ACQUIRE) == s) {
+      sv->probe[0] += 1;
+      for (int j = 0; j < 3; ++j) sv->probe[1 + j] += b->probe[j];
+      sv->probe[4] += (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now() - t0).count();
+      return true;
+    }
     // no wave of the current epoch running: start one (it takes the pending request)
     if (!sv->launched || __atomic_load_n(&b->alive, __ATOMIC_ACQUIRE) == 2 * sv->epoch + 2) {
       ++sv->epoch;
@@ -857,6 +873,21 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
   *state = nst;
   if (flags_out) *flags_out = fl;
   return fl ? RC_E_CHUNK : RC_OK;
+}
+
+// Internal (not in include/range_coder.h; tools/percall_native.cpp): the context's stream-service
+// timings since the last call, then reset: out[0] calls; out[1..3] the wave's 10-ns ticks summed
+// from seeing a request to its block in LDS, to the body done, to the results written back;
+// out[4] the host's wait from publishing the request to seeing its ack, in ns, summed.
+rc_status rc_svc_probe_(rc_ctx* ctx, uint64_t* out) {
+  if (!ctx || !out) return RC_E_ARG;
+  auto sv = svc_get(ctx);
+  std::lock_guard<std::mutex> lk(sv->mu);
+  for (int j = 0; j < 5; ++j) {
+    out[j] = sv->probe[j];
+    sv->probe[j] = 0;
+  }
+  return RC_OK;
 }
 
 // internal: free the context's staging block (called by rc_ctx_destroy)

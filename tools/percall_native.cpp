@@ -12,6 +12,9 @@
 
 #include "range_coder.hpp"
 
+// librc_amd's internal service timings (rc_resume.hip), not part of the public header
+extern "C" rc_status rc_svc_probe_(rc_ctx* ctx, uint64_t* out);
+
 class AdaptiveTable : public rc::PModel {  // examples/adaptive_impl.cpp's model
  public:
   AdaptiveTable() : c_(256, 1), cum_(256) { calc_cum(); }
@@ -83,6 +86,8 @@ int main(int argc, char** argv) {
   const std::vector<uint8_t> code = enc.finish();
   const double enc_us = (now_us() - t0) / n - upd;
 
+  uint64_t pr[5];
+  rc_svc_probe_(rc::Context::default_context().get(), pr);  // (reset)
   AdaptiveTable dm;
   rc::Decoder dec(code);
   t0 = now_us();
@@ -95,6 +100,8 @@ int main(int argc, char** argv) {
     dm.update(s, i);
   }
   const double dec_us = (now_us() - t0) / n - upd;
+  rc_svc_probe_(rc::Context::default_context().get(), pr);
+  const double pc = pr[0] ? (double)pr[0] : 1.0;
   // encode() with its return value read at every call (encoder.rs:34-36): one flush, so one
   // GPU call, per symbol
   AdaptiveTable cm;
@@ -113,8 +120,11 @@ int main(int argc, char** argv) {
   const char* sv = getenv("RC_STREAM_SERVICE");
   std::printf("{\"n\": %llu, \"service\": %s, \"model_update_us\": %.3f, "
               "\"adaptive_encode_us\": %.3f, \"adaptive_encode_count_us\": %.3f, "
-              "\"adaptive_decode_us\": %.3f}\n",
+              "\"adaptive_decode_us\": %.3f, \"decode_service_calls\": %llu, "
+              "\"wave_to_lds_us\": %.3f, \"wave_to_body_done_us\": %.3f, "
+              "\"wave_to_written_us\": %.3f, \"host_wait_us\": %.3f}\n",
               (unsigned long long)n, (sv && sv[0] == '0') ? "false" : "true", upd, enc_us,
-              cnt_us, dec_us);
+              cnt_us, dec_us, (unsigned long long)pr[0], pr[1] / pc / 100.0, pr[2] / pc / 100.0,
+              pr[3] / pc / 100.0, pr[4] / pc / 1000.0);
   return 0;
 }
