@@ -514,7 +514,7 @@ char* stage_acquire(const rc_ctx* ctx, size_t bytes, char** dev, std::shared_ptr
 // then only the bytes written (two waits); below it one copy of the whole region is cheaper.
 constexpr u64 kTwoPhaseBytes = 256u << 10;
 
-// The context's stream service (host side): the mailbox, the device scratch, the wave's own
+// The context's stream service (host side): the mailbox, the wave's own
 // non-blocking stream.  Held under its mutex for a whole call, like the staging block.
 struct Svc {
   std::mutex mu;
