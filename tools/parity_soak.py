@@ -15,6 +15,16 @@ kernels specialise on:
           rare symbols of skewed models exercise both renormalisation loops), or runs of one
           symbol
   chunks  1 .. 3000 chunks, lengths 0 .. 70000 with ragged mixes (0, 1, 7, 4095, 65536, ...)
+A quarter of the iterations instead draw one of:
+  adaptive    the build-defined adaptive model (rc_model_create_adaptive) with random valid
+              parameters, 1 .. 300 ragged chunks, against orc_encode_adaptive chunk by chunk
+  stream-enc  1 .. 200 resumable streams of random (c, cum, total) triples, valid or not (the
+              reference's panics and endless loops become flags at the same symbol), one
+              rc_stream_encode call with finish, against orc_stream_encode: bytes, per-symbol
+              counts, state and flags
+  stream-dec  1 .. 200 streams, valid or garbage code, decoded under one random table (zero
+              frequencies, inconsistent cum) by rc_stream_decode, against orc_stream_decode:
+              symbols, state and flags
 Prints a progress line per iteration and one JSON summary line; exits 1 at the first mismatch
 (after printing what differed).  The oracle is the checker here, never the thing measured.
 
@@ -118,6 +128,141 @@ def draw_data(rng, c, total_len):
     return out, how
 
 
+def adaptive_iteration(rng):
+    n_alpha = int(rng.choice([1, 2, 17, 100, 256, int(rng.integers(1, 257))]))
+    inc = int(rng.choice([1, 5, 32, 255, int(rng.integers(1, 256))]))
+    period = 1 << int(rng.integers(0, 9))
+    lo, hi = n_alpha + inc * period, 65535 - inc * period
+    if lo > hi:
+        inc, period = 32, 256
+        lo, hi = n_alpha + inc * period, 65535 - inc * period
+    limit = int(rng.integers(lo, hi + 1))
+    n = int(rng.choice([1, 7, 64, 65, int(rng.integers(1, 301))]))
+    lens = rng.choice([0, 1, 2, 63, 64, 65, 4096, int(rng.integers(0, 20001))], n).astype(np.int64)
+    s_exp = float(rng.uniform(0.0, 2.0))
+    w = 1.0 / np.arange(1, n_alpha + 1) ** s_exp
+    data = rng.choice(n_alpha, int(lens.sum()), p=w / w.sum()).astype(np.uint8)
+    sym_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    caps = np.array([rc.slot_capacity(int(L), 16) for L in lens], np.int64)
+    out_off = np.concatenate([[0], np.cumsum(caps)]).astype(np.int64)
+    m = rc.AdaptiveModel(n_alpha, inc, limit, period)
+    d_out = torch.zeros(int(out_off[-1]) + 16, dtype=torch.uint8, device="cuda")
+    ol, fe = rc.encode_batch(m, torch.from_numpy(np.concatenate([data, [0]]).astype(np.uint8)).cuda(),
+                             torch.from_numpy(sym_off).cuda(), d_out, torch.from_numpy(out_off).cuda())
+    dec = torch.zeros(int(sym_off[-1]) + 16, dtype=torch.uint8, device="cuda")
+    fd = rc.decode_batch(m, d_out, torch.from_numpy(out_off[:-1].copy()).cuda(), ol, dec,
+                         torch.from_numpy(sym_off).cuda())
+    torch.cuda.synchronize()
+    g_out, g_len, g_fe = d_out.cpu().numpy(), ol.cpu().numpy(), fe.cpu().numpy()
+    bad = []
+    for k in range(n):
+        f, want, L = cpu.encode_adaptive(n_alpha, inc, limit, period, data[sym_off[k]:sym_off[k + 1]])
+        a = int(out_off[k])
+        if f != int(g_fe[k]) or L != int(g_len[k]) or bytes(g_out[a:a + L]) != want:
+            bad.append(f"adaptive chunk {k}")
+            break
+    if not bad and ((fd.cpu().numpy() != 0).any() or
+                    not np.array_equal(dec.cpu().numpy()[: int(sym_off[-1])], data)):
+        bad.append("adaptive decode")
+    m.close()
+    return f"adaptive n={n_alpha} inc={inc} limit={limit} period={period}", n, int(lens.sum()), \
+        int(g_len.sum()), bad
+
+
+def random_triples(rng, n):
+    t = np.empty((n, 3), np.uint64)
+    for i in range(n):
+        total = int(rng.choice([256, 65536, int(rng.integers(1, 1 << 32))]))
+        c = int(rng.integers(1, total + 1)) if rng.random() < 0.97 else int(rng.integers(0, 1 << 32))
+        cum = int(rng.integers(0, total - min(c, total) + 1)) if rng.random() < 0.97 else \
+            int(rng.integers(0, 1 << 32))
+        t[i] = (c, cum, total if rng.random() < 0.995 else 0)
+    return t.astype(np.uint32)
+
+
+def stream_enc_iteration(rng):
+    ns = int(rng.integers(1, 201))
+    streams = [random_triples(rng, int(rng.choice([0, 1, 5, int(rng.integers(0, 2001))])))
+               for _ in range(ns)]
+    lens = np.array([len(t) for t in streams], np.int64)
+    sym_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    trip = np.concatenate([t.reshape(-1) for t in streams] + [np.zeros(3, np.uint32)])
+    caps = 12 * lens + 8
+    out_off = np.concatenate([[0], np.cumsum(caps)]).astype(np.int64)
+    states = rc.stream_states(ns)
+    out = torch.zeros(int(out_off[-1]) + 16, dtype=torch.uint8, device="cuda")
+    nb = torch.zeros(max(int(sym_off[-1]), 1), dtype=torch.uint8, device="cuda")
+    ctx = rc.default_context(0)
+    ol, fl = rc.stream_encode_batch(ctx, states, torch.from_numpy(trip.view(np.int32)).cuda(),
+                                    torch.from_numpy(sym_off).cuda(), out,
+                                    torch.from_numpy(out_off).cuda(), nbytes=nb, finish=True)
+    torch.cuda.synchronize()
+    h, ol, nbh = out.cpu().numpy(), ol.cpu().numpy(), nb.cpu().numpy()
+    stt = states.cpu().numpy().view(np.uint64)
+    bad = []
+    for k, t in enumerate(streams):
+        st = cpu.Stream.fresh()
+        f, b, cnt = cpu.stream_encode(st, t, finish=True)
+        lo, r, d, pos, n, fs = (int(x) for x in stt[k])
+        got = h[out_off[k]: out_off[k] + ol[k]].tobytes()
+        tup = st.tuple()
+        if got != b or nbh[sym_off[k]: sym_off[k] + len(cnt)].tolist() != cnt.tolist() or \
+                (lo, r, pos, n, fs & 0xFFFFFFFF, fs >> 32) != (tup[0], tup[1], tup[3], tup[4],
+                                                               tup[5], tup[6]):
+            bad.append(f"stream encode {k}")
+            break
+    return f"stream-enc streams={ns}", ns, int(lens.sum()), int(ol.sum()), bad
+
+
+def stream_dec_iteration(rng):
+    na = int(rng.choice([1, 2, 40, 256, int(rng.integers(1, 257))]))
+    c = np.array([int(rng.choice([0, 1, int(rng.integers(1, 900))])) for _ in range(na)], np.uint32)
+    if c.sum() == 0:
+        c[0] = 1
+    cum = np.concatenate([[0], np.cumsum(c.astype(np.uint64))[:-1]]).astype(np.uint32)
+    total = int(c.sum())
+    consistent = rng.random() < 0.7
+    tc, tcum, ttot = c.copy(), cum.copy(), total
+    if not consistent:  # an inconsistent table, as the reference decodes it anyway
+        tcum = rng.integers(0, max(total, 1) + 1, na).astype(np.uint32)
+        ttot = int(rng.choice([total, int(rng.integers(0, 1 << 32))]))
+    ns = int(rng.integers(1, 201))
+    codes = []
+    live = np.flatnonzero(c)
+    for k in range(ns):
+        if rng.random() < 0.5:
+            syms = live[rng.integers(0, len(live), int(rng.integers(0, 600)))].astype(np.uint8)
+            codes.append(cpu.encode(c, cum, total, syms)[1])
+        else:
+            codes.append(rng.integers(0, 256, int(rng.integers(0, 120))).astype(np.uint8).tobytes())
+    m = int(rng.integers(0, 700))
+    clen = np.array([len(x) for x in codes], np.int64)
+    coff = np.concatenate([[0], np.cumsum(clen)[:-1]]).astype(np.int64)
+    blob = np.frombuffer(b"".join(codes) + b"\0" * 16, np.uint8)
+    states = rc.stream_states(ns)
+    sym_off = (np.arange(ns + 1) * m).astype(np.int64)
+    syms = torch.zeros(ns * m + 16, dtype=torch.uint8, device="cuda")
+    ctx = rc.default_context(0)
+    rc.stream_decode_batch(ctx, torch.from_numpy(tc.view(np.int32)).cuda(),
+                           torch.from_numpy(tcum.view(np.int32)).cuda(), ttot, states,
+                           torch.from_numpy(blob.copy()).cuda(), torch.from_numpy(coff).cuda(),
+                           torch.from_numpy(clen).cuda(), syms, torch.from_numpy(sym_off).cuda())
+    torch.cuda.synchronize()
+    stt = states.cpu().numpy().view(np.uint64)
+    h = syms.cpu().numpy()
+    bad = []
+    for k, code in enumerate(codes):
+        st = cpu.Stream.fresh()
+        f, s = cpu.stream_decode(st, tc, tcum, ttot, code, m)
+        lo, r, d, pos, n, fs = (int(x) for x in stt[k])
+        if h[k * m: k * m + n].tolist() != s.tolist() or \
+                (lo, r, d, pos, n, fs & 0xFFFFFFFF) != st.tuple()[:6]:
+            bad.append(f"stream decode {k}")
+            break
+    return (f"stream-dec streams={ns} n_alpha={na} {'consistent' if consistent else 'inconsistent'}",
+            ns, ns * m, int(clen.sum()), bad)
+
+
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 240.0
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 20260518
@@ -127,6 +272,23 @@ def main():
     it = chunks = syms_total = bytes_total = 0
     kinds = {}
     while time.time() < t_end:
+        other = rng.random()
+        if other < 0.25:
+            fn = (adaptive_iteration if other < 0.1 else
+                  stream_enc_iteration if other < 0.175 else stream_dec_iteration)
+            name, n, nsym, nbytes, bad = fn(rng)
+            it += 1
+            chunks += n
+            syms_total += nsym
+            bytes_total += nbytes
+            key = name.split()[0]
+            kinds[key] = kinds.get(key, 0) + 1
+            print(f"iter {it}: {name} -> {'ok' if not bad else 'MISMATCH ' + ', '.join(bad)}",
+                  flush=True)
+            if bad:
+                print(json.dumps({"mismatch": bad, "iteration": it, "seed": seed, "draw": name}))
+                return 1
+            continue
         name, c, cum, total = draw_model(rng)
         lens = draw_lengths(rng)
         data, how = draw_data(rng, c, int(lens.sum()))
