@@ -8,6 +8,9 @@
 //   4  as 2, polling with s_sleep 0 instead of 1
 //   5  as 2, with seq and the request in fine-grained device memory the host writes through the
 //      BAR (the ack and results still in host memory); its own JSON line, after the others
+//   6  as 2, polling with relaxed loads (no cache invalidate per poll) and one acquire fence
+//      after the request is seen
+//   7  as 6, with four polls in flight (a new load issued as the oldest is checked)
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench_mailbox tools/ubench_mailbox.hip
 //   tools/ubench_mailbox [n]   -> one JSON line, microseconds per call
 #include <hip/hip_runtime.h>
@@ -31,6 +34,9 @@ struct alignas(64) Box {
 __device__ __forceinline__ u32 acq(const u32* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ u32 rlx(const u32* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 template <int V>
 __global__ __launch_bounds__(64) void k_mailbox(Box* box, Box* resp, u32 n, u32* sink) {
@@ -40,8 +46,38 @@ __global__ __launch_bounds__(64) void k_mailbox(Box* box, Box* resp, u32 n, u32*
   u32 acc = 0;
   for (u32 i = 1; i <= n; ++i) {
     u64 polls = 0;
-    for (;;) {
-      const u32 s = __builtin_amdgcn_readfirstlane(acq(&box->seq));
+    if (V == 7) {
+      u32 a0 = rlx(&box->seq);
+      __builtin_amdgcn_s_sleep(1);
+      u32 a1 = rlx(&box->seq);
+      __builtin_amdgcn_s_sleep(1);
+      u32 a2 = rlx(&box->seq);
+      __builtin_amdgcn_s_sleep(1);
+      u32 a3 = rlx(&box->seq);
+      for (;;) {
+        if (__builtin_amdgcn_readfirstlane(a0) == i) break;
+        a0 = rlx(&box->seq);
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_readfirstlane(a1) == i) break;
+        a1 = rlx(&box->seq);
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_readfirstlane(a2) == i) break;
+        a2 = rlx(&box->seq);
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_readfirstlane(a3) == i) break;
+        a3 = rlx(&box->seq);
+        __builtin_amdgcn_s_sleep(1);
+        if ((++polls & 15) == 0 &&
+            (polls > (1ull << 20) || __builtin_amdgcn_readfirstlane(rlx(&box->stop)))) {
+          sink[0] = 0xDEAD;
+          return;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
+    for (; V != 7;) {
+      const u32 s = __builtin_amdgcn_readfirstlane(V == 6 ? rlx(&box->seq) : acq(&box->seq));
+      if (V == 6 && s == i) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       if (s == i) break;
       if (++polls > (1ull << 22) || __builtin_amdgcn_readfirstlane(acq(&box->stop))) {
         sink[0] = 0xDEAD;  // (the host gave up: leave)
@@ -116,8 +152,10 @@ int main(int argc, char** argv) {
   const double v0 = run<0>(H, D, H, D, sink, n), v1 = run<1>(H, D, H, D, sink, n);
   const double v2 = run<2>(H, D, H, D, sink, n), v3 = run<3>(H, D, H, D, sink, n);
   const double v4 = run<4>(H, D, H, D, sink, n);
+  const double v6 = run<6>(H, D, H, D, sink, n), v7 = run<7>(H, D, H, D, sink, n);
   printf("{\"n\": %u, \"pingpong_us\": %.3f, \"burst_read_us\": %.3f, \"write_back_us\": %.3f, "
-         "\"relaxed_ack_us\": %.3f, \"sleep0_us\": %.3f}\n", n, v0, v1, v2, v3, v4);
+         "\"relaxed_ack_us\": %.3f, \"sleep0_us\": %.3f, \"relaxed_poll_us\": %.3f, "
+         "\"four_polls_in_flight_us\": %.3f}\n", n, v0, v1, v2, v3, v4, v6, v7);
   fflush(stdout);
   if (argc > 2 && !strcmp(argv[2], "vram")) {
     void* vb = nullptr;
