@@ -430,7 +430,8 @@ class Decoder {
       const size_t idx = pm.find_index(*this);  // reads range_coder() / data() at this symbol
       if (idx != PModel::kCanonical) return decode_index(pm, idx);
     }
-    Table t = table_of(pm);
+    table_of(pm, tmp_);  // (into reused vectors: no allocation per call)
+    Table& t = tmp_;
     const bool same = have_ && t == sig_;
     if (same && bpos_ < buf_.size()) {
       ++taken_;
@@ -442,14 +443,15 @@ class Decoder {
     uint64_t n = block_;
     if (limit_ != ~0ull) n = std::max<uint64_t>(1, std::min<uint64_t>(n, limit_ - taken_));
     const rc_stream_state start = st;
-    std::vector<uint8_t> out(n);
+    std::vector<uint8_t>& out = spare_;  // (reused: swapped with buf_ below)
+    out.resize(n);
     const uint32_t fl = run(st, t, n, out.data());
     out.resize(st.n - start.n);
     start_ = start;
     end_ = st;
-    buf_ = std::move(out);
+    buf_.swap(out);
     bpos_ = 0;
-    sig_ = std::move(t);
+    std::swap(sig_, t);  // (member-wise: the vectors swap their storage)
     have_ = true;
     err_ = fl;
     if (buf_.empty()) decode_error(start, sig_, fl);
@@ -507,8 +509,7 @@ class Decoder {
     throw_flags(fl ? fl : RC_F_CORRUPT, where);
     throw RangeCoderError(where);
   }
-  static Table table_of(const PModel& pm) {
-    Table t;
+  static void table_of(const PModel& pm, Table& t) {
     const size_t n = pm.alphabet_count();
     t.c.resize(n);
     t.cum.resize(n);
@@ -517,7 +518,6 @@ class Decoder {
       t.cum[i] = pm.cum_freq(i);
     }
     t.total = pm.total_freq();
-    return t;
   }
   uint32_t run(rc_stream_state& st, const Table& t, uint64_t n, uint8_t* out) const {
     uint32_t fl = 0;
@@ -552,7 +552,8 @@ class Decoder {
   mutable rc_stream_state start_ = RC_STREAM_STATE_INIT;
   rc_stream_state end_ = RC_STREAM_STATE_INIT;
   mutable size_t bpos_ = 0;
-  Table sig_;
+  Table sig_, tmp_;                // the table of the decoded-ahead block; the caller's, read now
+  std::vector<uint8_t> spare_;     // the next block's symbols before they replace buf_
   bool have_ = false;
   uint32_t err_ = 0;
   uint64_t block_ = 1, taken_ = 0;

@@ -545,9 +545,20 @@ bool svc_enabled() {
 }
 
 std::shared_ptr<Svc> svc_get(const rc_ctx* ctx) {
+  // (the calling thread's last context, without the global lock and map: a per-symbol caller
+  // comes here at every call; a context destroyed since, or a new one at the same address,
+  // finds its entry dead or gone and looks it up again)
+  thread_local const rc_ctx* last_ctx = nullptr;
+  thread_local std::weak_ptr<Svc> last_sv;
+  if (ctx == last_ctx) {
+    std::shared_ptr<Svc> sv = last_sv.lock();
+    if (sv && !__atomic_load_n(&sv->dead, __ATOMIC_ACQUIRE)) return sv;
+  }
   std::lock_guard<std::mutex> g(g_svc_mu);
   auto& slot = g_svcs[ctx];
   if (!slot) slot = std::make_shared<Svc>();
+  last_ctx = ctx;
+  last_sv = slot;
   return slot;
 }
 
@@ -570,9 +581,10 @@ void svc_teardown(Svc* sv) {
 // Returns false (and the call takes the launch path) when the service is off, broken, or
 // cannot be set up; RC_E_DEVICE in *err when the wave did not answer.
 template <class Fill>
-bool svc_call(const rc_ctx* ctx, Svc* sv, Fill fill, rc_status* err) {
+bool svc_call(const rc_ctx* ctx, Svc* sv, int dev, Fill fill, rc_status* err) {
   if (sv->dead || sv->broken) return false;
   if (!sv->box) {
+    Dev g(dev);
     void* hb = nullptr;
     if (hipHostMalloc(&hb, sizeof(SvcBox) + SVC_BLOCK,
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
@@ -606,6 +618,7 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, Fill fill, rc_status* err) {
     }
     // no wave of the current epoch running: start one (it takes the pending request)
     if (!sv->launched || __atomic_load_n(&b->alive, __ATOMIC_ACQUIRE) == 2 * sv->epoch + 2) {
+      Dev g(dev);
       ++sv->epoch;
       hipLaunchKernelGGL(k_stream_service, dim3(1), dim3(RWG), 0, sv->stream, sv->dbox_host,
                          sv->epoch, (u64)SVC_IDLE_MS * 100000ull,
@@ -689,7 +702,6 @@ rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint3
     if (flags_out) *flags_out = RC_F_CAPACITY;
     return RC_E_CAPACITY;
   }
-  Dev g(dev);
   // block: state | offsets (4 x u64) | out_len | flags | triples || nbytes | out
   const size_t o_off = 64, o_len = o_off + 32, o_fl = o_len + 16, o_tr = o_fl + 16;
   const size_t o_nb = o_tr + ((12 * n + 15) & ~15ull), o_out = o_nb + ((n + 15) & ~15ull);
@@ -698,7 +710,7 @@ rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint3
     auto sv = svc_get(ctx);
     std::lock_guard<std::mutex> slk(sv->mu);
     rc_status err = RC_OK;
-    if (svc_call(ctx, sv.get(), [&](char* h, SvcBox* b) {
+    if (svc_call(ctx, sv.get(), dev, [&](char* h, SvcBox* b) {
           memcpy(h, state, sizeof *state);
           const u64 offs[4] = {0, n, 0, need};
           memcpy(h + o_off, offs, sizeof offs);
@@ -729,6 +741,7 @@ rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint3
       return fl ? RC_E_CHUNK : RC_OK;
     }
   }
+  Dev g(dev);  // (the service path makes no HIP call but its wave's launch, guarded there)
   char* d = nullptr;
   std::shared_ptr<Stage> keep;
   std::unique_lock<std::mutex> lk;
@@ -794,7 +807,6 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
   const u64 p0 = state->stage == 0 ? 0 : state->pos;
   if (p0 > code_len) return RC_E_ARG;
   const u64 wlen = std::min<u64>(code_len - p0, (state->stage == 0 ? 8 : 0) + 12 * n);
-  Dev g(dev);
   // block: state | offsets: code_off, code_len, sym_off[0..1] | flags | c | cum | window || syms
   const size_t o_off = 64, o_fl = o_off + 32, o_c = o_fl + 16, o_cum = o_c + 1024;
   const size_t o_win = o_cum + 1024, o_sym = o_win + ((wlen + 15) & ~15ull);
@@ -803,7 +815,7 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
     auto sv = svc_get(ctx);
     std::lock_guard<std::mutex> slk(sv->mu);
     rc_status err = RC_OK;
-    if (svc_call(ctx, sv.get(), [&](char* h, SvcBox* b) {
+    if (svc_call(ctx, sv.get(), dev, [&](char* h, SvcBox* b) {
           rc_stream_state rel = *state;
           rel.pos -= p0;  // the window starts at p0 (stage 0: at the stream start)
           memcpy(h, &rel, sizeof rel);
@@ -837,6 +849,7 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
       return fl ? RC_E_CHUNK : RC_OK;
     }
   }
+  Dev g(dev);
   char* d = nullptr;
   std::shared_ptr<Stage> keep;
   std::unique_lock<std::mutex> lk;
@@ -905,7 +918,7 @@ void rc_resume_release_(const rc_ctx* ctx) {
     if (sv) {
       std::lock_guard<std::mutex> lk(sv->mu);
       svc_teardown(sv.get());
-      sv->dead = true;
+      __atomic_store_n(&sv->dead, true, __ATOMIC_RELEASE);  // (svc_get's fast path reads it)
     }
   }
   std::shared_ptr<Stage> st;
