@@ -608,6 +608,7 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, int dev, Fill fill, rc_status* err) {
   const u32 s = sv->seq;
   __atomic_store_n(&b->seq, s, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
+  auto t_run = t0;  // (the last time the current epoch's wave was seen not running)
   for (u32 spin = 0;; ++spin) {
     if (__atomic_load_n(&b->ack, __ATOMIC_ACQUIRE) == s) {
       sv->probe[0] += 1;
@@ -631,7 +632,12 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, int dev, Fill fill, rc_status* err) {
       sv->launched = true;
     }
     if ((spin & 1023) == 1023) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      // The timeout runs only while the current epoch's wave runs: a wave still waiting for a
+      // CU (another long kernel holding the LDS it needs) is waited for, as a launch would be;
+      // a wave that cannot start because the device failed shows in the stream query below.
+      const auto now = std::chrono::steady_clock::now();
+      if (__atomic_load_n(&b->alive, __ATOMIC_ACQUIRE) != 2 * sv->epoch + 1) t_run = now;
+      if (now - t_run > std::chrono::seconds(10)) {
         svc_teardown(sv);  // (waits for the wave to leave: every exit is bounded)
         sv->broken = true;
         *err = RC_E_DEVICE;
