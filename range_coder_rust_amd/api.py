@@ -907,18 +907,21 @@ class Decoder:
         if not _canonical_find_index(pmodel):
             return self._decode_by_find_index(pmodel)
         sig = _table_of(pmodel)
-        if sig == self._sig and self._bpos < len(self._buf):
+        same = sig == self._sig
+        used = self._bpos == len(self._buf)
+        if same and not used:
             s = self._buf[self._bpos]
             self._bpos += 1
             self._taken += 1
             return int(s)
-        if sig == self._sig and self._err:  # the reference panics / hangs at this symbol
+        if same and self._err:  # the reference panics / hangs at this symbol
             _decode_error(self._end, sig, self._err, f"decode (symbol {self._taken})")
-        if sig == self._sig and self._bpos == len(self._buf):
-            self._block = min(2 * self._block, self.MAX_BLOCK)
+        self._block = min(2 * self._block, self.MAX_BLOCK) if same and used else 1
+        if used and self._bpos:  # (the block used up: its end state, as _here gives it, once)
+            st = self._copy(self._end)
+            st.flags = 0
         else:
-            self._block = 1
-        st = self._copy(self._here())
+            st = self._copy(self._here())
         n = self._block
         if self._limit is not None:
             n = max(1, min(n, self._limit - self._taken))
