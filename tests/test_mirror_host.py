@@ -6,7 +6,10 @@ reused buffers, large ones through numpy arrays), the decode-ahead blocks that d
 table holds, re-deriving the state when the caller's table changes or range_coder() / data() are
 asked mid-block, the find_index override path (pmodel.rs:12), and the reference's errors at the
 call that hits them.  Expected values come from oracle/ref_literal.py, the literal restatement.
-The GPU suite (tests/test_gpu_stream.py) runs the same surface on the kernels.
+The GPU suite (tests/test_gpu_stream.py) runs the same surface on the kernels.  The C++ mirror
+(include/range_coder.hpp) gets the same treatment: the examples (examples/*.cpp) are built with
+g++ against tests/native/oracle_backed_rc.cpp, which implements those two entry points over the
+oracle, and their output is checked as the GPU suite checks it.
 
 The fake reads the caller's buffers only inside the call, after allocating and filling scratch
 arrays of the same sizes, so a buffer the mirror let go of before the call (a temporary whose
@@ -239,3 +242,58 @@ def test_errors_at_the_reference_call():
     with pytest.raises(rc.RangeCoderError):
         for _ in range(16):
             dec.decode(t1)  # runs out of code bytes: decoder.rs:33 panics
+
+
+# ---- the C++ mirror (include/range_coder.hpp), built against the oracle-backed stand-in ----
+import os  # noqa: E402
+import subprocess  # noqa: E402
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def cpp_examples(tmp_path_factory):
+    d = tmp_path_factory.mktemp("cpp_mirror")
+    exes = {}
+    for name in ("sample_impl", "adaptive_impl", "find_index_impl"):
+        exe = str(d / name)
+        subprocess.run(["g++", "-O2", "-std=c++17", "-I" + os.path.join(_ROOT, "include"),
+                        os.path.join(_ROOT, "examples", name + ".cpp"),
+                        os.path.join(_ROOT, "tests", "native", "oracle_backed_rc.cpp"),
+                        "-x", "c", os.path.join(_ROOT, "oracle", "rc_oracle.c"),
+                        "-o", exe], check=True)
+        exes[name] = exe
+    return exes
+
+
+def test_cpp_sample_impl_on_cpu(cpp_examples):
+    r = subprocess.run([cpp_examples["sample_impl"]], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "output : 0x64475f8970365a2f83b20246c0" in r.stdout and "test passed" in r.stdout
+
+
+def _xorshift_syms(n, seed):  # examples/adaptive_impl.cpp's symbol generator
+    x, out, M = seed, [], (1 << 64) - 1
+    for _ in range(n):
+        x ^= (x << 13) & M
+        x ^= x >> 7
+        x ^= (x << 17) & M
+        r = x % 1000
+        out.append(r % 4 if r < 500 else (r % 32 if r < 800 else r % 256))
+    return out
+
+
+def test_cpp_caller_adaptive_model_on_cpu(cpp_examples):
+    n, seed = 3000, 5
+    r = subprocess.run([cpp_examples["adaptive_impl"], str(n), str(seed)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip() == R.encode_adaptive_stream(256, 32, 4000, 64,
+                                                        _xorshift_syms(n, seed)).hex()
+
+
+def test_cpp_find_index_on_cpu(cpp_examples):
+    r = subprocess.run([cpp_examples["find_index_impl"]], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "find_index called 16 times" in r.stdout and "test passed" in r.stdout
