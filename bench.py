@@ -1,24 +1,24 @@
 #!/usr/bin/env python3
 """Benchmark of the batched range coder hot path (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): 2^20 independent 64 KiB chunks per GPU, uniform-256 static
-PModel (c[i] = 1, total 256), synthetic symbols generated in HBM.  One step = encode every chunk
-(reference: Encoder::new + 65,536 x encode + finish, encoder.rs:14-46) then decode every chunk
+Headline, the same workload at every N (BASELINE.json configs[4]; at N = 1 it is configs[2]'s
+encode+decode at full size): one fixed stream of 2^20 independent 64 KiB chunks, Zipf(1.2)
+256-symbol static PModel (total 2^16), synthetic symbols generated in HBM, split into contiguous
+shards over the N ranks (strong scaling).  One step = encode every chunk of the shard (reference:
+Encoder::new + 65,536 x encode + finish, encoder.rs:14-46) then decode every chunk
 (Decoder::new + 65,536 x decode, decoder.rs:14-54), all inputs resident in HBM.
-value = symbols round-tripped / second over all ranks = N_sym / (t_enc + t_dec), Gsymbols/s.
+value = symbols round-tripped / second over all ranks = 2^36 / max-over-ranks step time.
 
-N > 1 (one process per GPU): `bench.py --gpus N` launches its N ranks itself (torch.distributed.run
-on 127.0.0.1, before any GPU call), or runs as one rank of an external torchrun whose WORLD_SIZE
-must equal N.  The N > 1 line is configs[4]: one fixed 64 GiB Zipf(1.2) stream of 2^20 x 64 KiB
-chunks split into contiguous shards over the ranks (strong scaling; chunks are independent
-streams, encoder.rs:48-55, so there is no data-path collective).  The uniform configs[1] load of
-2^20 chunks per rank (weak scaling) is reported beside it under extras.uniform_weak.  The
-torch.distributed process group (RCCL) carries only the barriers, the max-over-ranks of the timed
-region and the all-ranks-bit-exact flag (range_coder_rust_amd/shard.py).
+Chunks are independent streams (encoder.rs:48-55), so the shards need no data-path collective:
+the process group (RCCL) carries only the barriers, the max-over-ranks of the timed region and
+the all-ranks-bit-exact flag (range_coder_rust_amd/shard.py).  `bench.py --gpus N` launches its
+N ranks itself (torch.distributed.run on 127.0.0.1, before any GPU call), or runs as one rank of
+an external torchrun whose WORLD_SIZE must equal N.
 
-Also reported: the Zipf(1.2) configuration (configs[2]) on the same buffers, per-kernel times,
-the HBM roofline of the dominant kernel and a CPU baseline (the C oracle on the host cores,
-rank 0, N = 1 only, on a bounded sample).
+Extras at every N: the uniform configs[1] load (2^20 chunks per GPU, c = 1, total 256; weak
+scaling) and the adaptive configs[3] model.  At N = 1 also: the histogram / entropy report,
+the container and the host-resident (PCIe) legs on the headline's buffers, and a CPU baseline
+(the C oracle on the host cores, rank 0, on a bounded sample).
 """
 import argparse
 import json
@@ -42,14 +42,12 @@ def parse():
                    help="GPUs (ranks) of this node; default WORLD_SIZE or 1")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU")
-    p.add_argument("--global-chunks", type=int, default=None,
-                   help="shard this many chunks over the ranks instead (strong scaling); "
-                        "default 2^20 (configs[4]) when N > 1, else off")
+    p.add_argument("--chunks", type=int, default=1 << 20,
+                   help="uniform extra (configs[1], weak): chunks per GPU")
+    p.add_argument("--global-chunks", type=int, default=1 << 20,
+                   help="headline (configs[4], strong): chunks sharded over the ranks")
     p.add_argument("--chunk-bytes", type=int, default=65536)
-    p.add_argument("--config", choices=["uniform", "zipf"], default=None,
-                   help="default: uniform (configs[1]) at N = 1, zipf (configs[4]) at N > 1")
-    p.add_argument("--no-zipf", action="store_true", help="skip the secondary Zipf leg")
+    p.add_argument("--no-uniform", action="store_true", help="skip the uniform configs[1] leg")
     p.add_argument("--no-adaptive", action="store_true", help="skip the adaptive (C4) leg")
     p.add_argument("--no-model-build", action="store_true",
                    help="skip the histogram / entropy-report leg (on the Zipf inputs)")
@@ -384,13 +382,54 @@ def resolve_world(args):
     return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
+HEADLINE_MODEL = "Zipf(1.2) static (total 2^16)"
+
+
+def plan(world, rank, global_chunks=1 << 20, chunks_per_gpu=1 << 20, L=65536, uniform=True):
+    """What each rank runs.  The headline is ONE workload at every N (configs[4]; at N = 1 it is
+    configs[2]'s encode+decode at full size): the 2^20 x 64 KiB Zipf(1.2) stream, split into
+    contiguous shards over the ranks (strong scaling: the job's symbols are fixed, so a 1/2/4/8
+    curve of `value` is a speed-up curve).  The uniform configs[1] load (chunks_per_gpu per rank,
+    weak scaling) is an extra at every N, N = 1 included."""
+    from range_coder_rust_amd import shard
+    lo, hi = shard.shard_range(global_chunks, world, rank)
+    workload = (f"configs[4]: {global_chunks} x {L // 1024} KiB chunks sharded over {world} "
+                f"GPU(s), {HEADLINE_MODEL}, encode then decode, inputs resident in HBM")
+    return dict(lo=lo, n=hi - lo, n_all=global_chunks, scaling="strong", workload=workload,
+                weak_n=chunks_per_gpu if uniform else 0, weak_lo=rank * chunks_per_gpu)
+
+
+def kernel_stats(n_sym, code_bytes, ms):
+    """Gsym/s, algorithmic GB/s and HBM fraction of one kernel: encode reads the symbols and
+    writes the code, decode reads the code and writes the symbols."""
+    alg = n_sym + code_bytes
+    return dict(ms=ms, gsym_s=n_sym / ms / 1e6, gbps=alg / ms / 1e6,
+                frac=alg / ms / 1e6 / HBM_PEAK_GBPS, alg_bytes=alg)
+
+
+def traffic_for(path, key):
+    """(HBM bytes per launch, note) from tools/pmc_traffic.py's file, only when the entry was
+    profiled on this exact librc_amd.so (keyed by its sha256)."""
+    note = "no profile of this workload in " + os.path.relpath(path, ROOT)
+    try:
+        with open(path) as f:
+            tr = json.load(f)
+    except (OSError, ValueError):
+        return None, note
+    if key not in tr:
+        return None, note
+    from range_coder_rust_amd import _native
+    e = tr[key]
+    if e.get("lib_sha256") != lib_sha256(_native.LIB_PATH):
+        return None, f"stale: {e.get('round')} profiled another build of librc_amd.so; not reported"
+    return e["hbm_bytes_per_launch"], f"PMC, this build ({e.get('round')})"
+
+
 def main():
     args = parse()
     world, rank, local = resolve_world(args)
-    if args.config is None:
-        args.config = "zipf" if world > 1 else "uniform"
-    if args.global_chunks is None:
-        args.global_chunks = (1 << 20) if world > 1 else 0
+    P = plan(world, rank, args.global_chunks, args.chunks, args.chunk_bytes,
+             uniform=not args.no_uniform)
     import torch
     import torch.distributed as dist
 
@@ -406,93 +445,66 @@ def main():
             CTRL_DEVICE = "cpu"
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    dd = dist if world > 1 else None
 
     import range_coder_rust_amd as rc
-    from range_coder_rust_amd import synth
+    from range_coder_rust_amd import shard, synth
     ctx = rc.default_context(gpu)
 
-    from range_coder_rust_amd import shard
-    L = args.chunk_bytes
-    if args.global_chunks:
-        lo, hi = shard.shard_range(args.global_chunks, world, rank)
-        n, n_all, scaling = hi - lo, args.global_chunks, "strong"
-    else:
-        n = args.chunks
-        lo, n_all, scaling = rank * n, n * world, "weak"
-    # N > 1 also runs the weak uniform load (2^20 chunks per rank): one arena for both legs
-    weak_n = args.chunks if (world > 1 and args.global_chunks and not args.no_zipf) else 0
-    bufs = Leg.alloc(torch, torch.device("cuda", gpu), max(n, weak_n), L)
-    leg = Leg(torch, rc, synth, ctx, args.config, n, L, lo, bufs=bufs)
+    L, n, lo, n_all = args.chunk_bytes, P["n"], P["lo"], P["n_all"]
+    # one arena for every leg (each takes prefixes): the headline shard and the weak uniform load
+    bufs = Leg.alloc(torch, torch.device("cuda", gpu), max(n, P["weak_n"]), L)
+    leg = Leg(torch, rc, synth, ctx, "zipf", n, L, lo, bufs=bufs)
     res = run_leg(torch, dist, leg, args.steps, args.warmup, world)
-    n_sym_all = n_all * L
-    value = n_sym_all * args.steps / res["t"] / 1e9
+    value = n_all * L * args.steps / res["t"] / 1e9
 
-    # algorithmic bytes per launch: encode reads N symbols + writes the code, decode reads the
-    # code + writes N symbols; identical for both kernels
-    alg_bytes = n * L + res["code_bytes"]
-    kern = {
-        "encode": dict(ms=res["enc_ms"], gsym_s=n * L / res["enc_ms"] / 1e6,
-                       gbps=alg_bytes / res["enc_ms"] / 1e6),
-        "decode": dict(ms=res["dec_ms"], gsym_s=n * L / res["dec_ms"] / 1e6,
-                       gbps=alg_bytes / res["dec_ms"] / 1e6),
-    }
+    kern = {"encode": kernel_stats(n * L, res["code_bytes"], res["enc_ms"]),
+            "decode": kernel_stats(n * L, res["code_bytes"], res["dec_ms"])}
     dom = "decode" if res["dec_ms"] >= res["enc_ms"] else "encode"
-    # roofline.traffic: PMC-measured HBM bytes of this exact library build only (the entry is
-    # keyed to the sha256 of the librc_amd.so it was profiled on; tools/pmc_traffic.py)
-    traffic, traffic_note = None, "no profile of this workload in " + os.path.relpath(args.traffic, ROOT)
-    try:
-        with open(args.traffic) as f:
-            tr = json.load(f)
-        key = f"{args.config}:{n}:{L}:{dom}"
-        if key in tr:
-            from range_coder_rust_amd import _native
-            if tr[key].get("lib_sha256") == lib_sha256(_native.LIB_PATH):
-                traffic = tr[key]["hbm_bytes_per_launch"]
-                traffic_note = f"PMC, this build ({tr[key].get('round')})"
-            else:
-                traffic_note = (f"stale: {tr[key].get('round')} profiled another build of "
-                                f"librc_amd.so; not reported")
-    except (OSError, ValueError, KeyError):
-        traffic = None
+    # roofline.traffic: PMC-measured HBM bytes of this exact library build only
+    traffic, traffic_note = traffic_for(args.traffic, f"zipf:{n}:{L}:{dom}")
     achieved = kern[dom]["gbps"]
     roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBPS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic,
-                    traffic_source=traffic_note, kernel=dom,
-                    alg_bytes_per_launch=alg_bytes)
+                    traffic_source=traffic_note, kernel=f"{dom} (Zipf(1.2), LUT 4)",
+                    alg_bytes_per_launch=kern[dom]["alg_bytes"])
+    # N > 1: achieved / peak above is one rank's kernel against one GPU; the aggregate is every
+    # rank's algorithmic bytes over the slowest rank's kernel time against N GPUs' peak
+    alg_all = shard.sum_over_ranks(kern[dom]["alg_bytes"], dd, device=CTRL_DEVICE)
+    ms_max = shard.max_over_ranks(kern[dom]["ms"], dd, device=CTRL_DEVICE)
+    roofline["scope"] = "per GPU (rank 0's kernel vs one GPU's peak)"
+    roofline["aggregate"] = dict(achieved=round(alg_all / ms_max / 1e6, 2),
+                                 peak=HBM_PEAK_GBPS * world,
+                                 frac=round(alg_all / ms_max / 1e6 / (HBM_PEAK_GBPS * world), 4),
+                                 n_gpus=world)
 
     extras = {}
-    if weak_n:
-        u = Leg(torch, rc, synth, ctx, "uniform", weak_n, L, rank * weak_n, bufs=bufs)
-        ur = run_leg(torch, dist, u, max(2, args.steps // 2), 1, world)
+    if P["weak_n"]:  # configs[1]: the uniform model, 2^20 chunks on every rank
+        wn = P["weak_n"]
+        u = Leg(torch, rc, synth, ctx, "uniform", wn, L, P["weak_lo"], bufs=bufs)
+        us = max(2, args.steps // 2)
+        ur = run_leg(torch, dist, u, us, 1, world)
+        ue = kernel_stats(wn * L, ur["code_bytes"], ur["enc_ms"])
+        ud = kernel_stats(wn * L, ur["code_bytes"], ur["dec_ms"])
+        utr, utr_note = traffic_for(args.traffic, f"uniform:{wn}:{L}:decode")
         extras["uniform_weak"] = dict(
-            workload=f"configs[1] on every rank: {weak_n} x {L // 1024} KiB chunks per GPU, "
-                     f"uniform-256 static model (weak scaling)",
-            value=round(weak_n * world * L * max(2, args.steps // 2) / ur["t"] / 1e9, 3),
-            encode_gsym_s=round(weak_n * L / ur["enc_ms"] / 1e6, 3),
-            decode_gsym_s=round(weak_n * L / ur["dec_ms"] / 1e6, 3),
+            workload=f"configs[1] on every rank: {wn} x {L // 1024} KiB chunks per GPU, "
+                     f"uniform-256 static model (c = 1, total 256; weak scaling)",
+            value=round(wn * world * L * us / ur["t"] / 1e9, 3),
+            encode_gsym_s=round(ue["gsym_s"], 3), decode_gsym_s=round(ud["gsym_s"], 3),
+            encode_ms=round(ue["ms"], 3), decode_ms=round(ud["ms"], 3),
+            bytes_per_symbol=round(ur["code_bytes"] / (wn * L), 5),
+            roofline_frac_encode=round(ue["frac"], 4), roofline_frac_decode=round(ud["frac"], 4),
+            decode_traffic=utr, decode_traffic_source=utr_note,
             bit_exact_round_trip=ur["ok"])
-    if not args.no_zipf and args.config == "uniform":
-        z = Leg(torch, rc, synth, ctx, "zipf", n, L, lo, bufs=bufs)
-        zr = run_leg(torch, dist, z, max(2, args.steps // 2), 1, world)
-        zb = n * L + zr["code_bytes"]
-        extras["zipf1.2"] = dict(
-            workload=f"configs[2] (and configs[4] at N = {world}): {n} x {L // 1024} KiB chunks "
-                     f"per GPU, Zipf(1.2) static model",
-            value=round(n_sym_all * max(2, args.steps // 2) / zr["t"] / 1e9, 3),
-            encode_gsym_s=round(n * L / zr["enc_ms"] / 1e6, 3),
-            decode_gsym_s=round(n * L / zr["dec_ms"] / 1e6, 3),
-            encode_ms=round(zr["enc_ms"], 3), decode_ms=round(zr["dec_ms"], 3),
-            bytes_per_symbol=round(zr["code_bytes"] / (n * L), 5),
-            roofline_frac_encode=round(zb / zr["enc_ms"] / 1e6 / HBM_PEAK_GBPS, 4),
-            roofline_frac_decode=round(zb / zr["dec_ms"] / 1e6 / HBM_PEAK_GBPS, 4),
-            bit_exact_round_trip=zr["ok"])
+    if world == 1:
         if not args.no_model_build:
-            extras["model_build"] = model_build_leg(torch, rc, z, zr["code_bytes"])
+            extras["model_build"] = model_build_leg(torch, rc, leg, res["code_bytes"])
         if not args.no_container:
-            extras["container"] = container_leg(torch, rc, z)
-        if not args.no_host_stream and world == 1:
-            extras["host_stream"] = host_stream_leg(torch, rc, z, 131072)
-    if not args.no_adaptive and args.config == "uniform" and L % 16384 == 0:
+            extras["container"] = container_leg(torch, rc, leg)
+        if not args.no_host_stream:
+            extras["host_stream"] = host_stream_leg(torch, rc, leg, 131072)
+    if not args.no_adaptive and L % 16384 == 0:
         La = 16384
         na = n * (L // La)
         a = Leg(torch, rc, synth, ctx, "adaptive", na, La, lo * (L // La), bufs=bufs)
@@ -519,11 +531,6 @@ def main():
     ok_all = res["ok"] and all(e.get("bit_exact_round_trip", True) for e in extras.values()
                                if isinstance(e, dict))
     if rank == 0:
-        model = ("uniform-256 static (c=1, total=256)" if args.config == "uniform"
-                 else "Zipf(1.2) static (total 2^16)")
-        shape = (f"configs[4]: {n_all} x {L // 1024} KiB chunks sharded over {world} GPU(s)"
-                 if args.global_chunks else f"configs[1]: {n} x {L // 1024} KiB chunks per GPU")
-        workload = f"{shape}, {model}, encode then decode, inputs resident in HBM"
         line = {
             "metric": "Gsymbols/s encode+decode, 256-sym static model, 64KiB chunks, 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -533,11 +540,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(res["t"] / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": scaling,
+            "scaling": P["scaling"],
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic",
-            "config": {"workload": workload,
+            "config": {"workload": P["workload"],
                        "chunks_per_gpu": n, "chunks_total": n_all, "chunk_symbols": L,
                        "alphabet": 256,
                        "total_freq": int(leg.total), "parallelism": f"chunk-shard x{world}"},
@@ -547,6 +554,7 @@ def main():
             "decode_gsym_s": round(kern["decode"]["gsym_s"], 3),
             "encode_ms": round(res["enc_ms"], 3),
             "decode_ms": round(res["dec_ms"], 3),
+            "roofline_frac_encode": round(kern["encode"]["frac"], 4),
             "bytes_per_symbol": round(res["code_bytes"] / (n * L), 5),
             "bit_exact_round_trip": res["ok"],
             "extras": extras,

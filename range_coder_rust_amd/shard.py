@@ -64,6 +64,16 @@ def max_over_ranks(value, dist=None, device=None):
     return float(t.item())
 
 
+def sum_over_ranks(value, dist=None, device=None):
+    """The sum of an integer count over the ranks (bench: every rank's algorithmic bytes)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return int(value)
+    import torch
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
 def all_ranks_true(flag, dist=None, device=None):
     """True when `flag` holds on every rank (an all-reduce MIN of one int)."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:

@@ -48,6 +48,29 @@ def test_exclusive_scan():
     assert off.size == 0 and total == 0
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_headline_is_one_workload_at_every_n(world):
+    """bench.py's headline is configs[4] at every N: the same stream, only the shard count in
+    the workload string changes, and the shards cover the global chunks exactly once."""
+    import bench
+    one = bench.plan(1, 0)
+    assert one["n"] == one["n_all"] == 1 << 20 and one["scaling"] == "strong"
+    assert "Zipf(1.2)" in one["workload"] and "configs[4]" in one["workload"]
+    plans = [bench.plan(world, r) for r in range(world)]
+    for p in plans:
+        assert p["workload"] == one["workload"].replace("over 1 GPU(s)", f"over {world} GPU(s)")
+        assert p["n_all"] == one["n_all"] and p["scaling"] == "strong"
+        # the uniform configs[1] extra keeps 2^20 chunks per GPU (weak)
+        assert p["weak_n"] == 1 << 20
+    assert sum(p["n"] for p in plans) == 1 << 20
+    assert [p["lo"] for p in plans] == [shard.shard_range(1 << 20, world, r)[0]
+                                         for r in range(world)]
+
+
+def test_sum_over_ranks_single_process():
+    assert shard.sum_over_ranks(7) == 7
+
+
 def _table():
     c, cum, total = synth.zipf_table()
     return c, cum, total, synth.inverse_cdf(c)
@@ -77,6 +100,8 @@ def _worker(rank, world, port, q):
         code, lens = _encode_range(lo, hi)
         base, total = shard.global_code_offset(len(code), dist)
         t = shard.max_over_ranks(0.25 * (rank + 1), dist)
+        # (bench.py's aggregate roofline: every rank's bytes summed)
+        assert shard.sum_over_ranks(len(code), dist) == total
         q.put((rank, lo, hi, base, total, t, code))
     finally:
         dist.destroy_process_group()
