@@ -65,9 +65,12 @@ def parse():
 
 
 def table(cfg):
-    """The static model of cfg, or for "adaptive" the Zipf table its data is drawn from."""
+    """The static model of cfg, or for "adaptive" / "adaptive128" the Zipf table its data is
+    drawn from (over 256 / 128 symbols)."""
     from range_coder_rust_amd import synth
-    return synth.uniform_table() if cfg == "uniform" else synth.zipf_table()
+    if cfg == "uniform":
+        return synth.uniform_table()
+    return synth.zipf_table(n=128) if cfg == "adaptive128" else synth.zipf_table()
 
 
 class Leg:
@@ -76,8 +79,8 @@ class Leg:
     def __init__(self, torch, rc, synth, ctx, cfg, n, L, first_chunk, bufs=None):
         c, cum, total = table(cfg)
         self.cfg, self.n, self.L = cfg, n, L
-        if cfg == "adaptive":  # configs[3]: the C4 model over Zipf(1.2) data
-            self.model = rc.AdaptiveModel(256, **rc.ADAPTIVE_DEFAULTS, ctx=ctx)
+        if cfg.startswith("adaptive"):  # configs[3]: the C4 model over Zipf(1.2) data
+            self.model = rc.AdaptiveModel(len(c), **rc.ADAPTIVE_DEFAULTS, ctx=ctx)
             cap = rc.slot_capacity(L, 6.0, slack=1.02)  # Zipf(1.2) codes at ~5.4 bits/symbol
         else:
             self.model = rc.StaticModel(c, cum, total, ctx=ctx)
@@ -518,6 +521,18 @@ def main():
             encode_ms=round(ar["enc_ms"], 3), decode_ms=round(ar["dec_ms"], 3),
             bytes_per_symbol=round(ar["code_bytes"] / (na * La), 5),
             bit_exact_round_trip=ar["ok"])
+        # the same model over a 128-symbol alphabet: its decoder's 127-node tree (16 KiB of
+        # LDS per wave instead of 32) lets twice the waves share a CU
+        a = Leg(torch, rc, synth, ctx, "adaptive128", na, La, lo * (L // La), bufs=bufs)
+        ar8 = run_leg(torch, dist, a, max(2, args.steps // 2), 1, world)
+        extras["adaptive_c4_128"] = dict(
+            workload=f"configs[3] with a 128-symbol alphabet: {na} x 16 KiB chunks per GPU, "
+                     f"Zipf(1.2) data over 128 symbols",
+            encode_gsym_s=round(na * La / ar8["enc_ms"] / 1e6, 3),
+            decode_gsym_s=round(na * La / ar8["dec_ms"] / 1e6, 3),
+            decode_vs_256=round(ar["dec_ms"] / ar8["dec_ms"], 3),
+            bytes_per_symbol=round(ar8["code_bytes"] / (na * La), 5),
+            bit_exact_round_trip=ar8["ok"])
 
     cpu_b = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -73,6 +73,20 @@ typedef int rc_status;
 #define RC_MAX_CHUNKS (1u << 28)
 
 typedef struct rc_ctx rc_ctx;     /* one device + one stream; use one per host thread */
+
+/* Environment.  rc_ctx_create reads these switches once and the context keeps them; nothing
+ * reads the environment per launch or per call (changing a variable affects contexts created
+ * after the change only).  Unset is the default.
+ *   RC_PRIO=off             wave priorities off (every launch oldest-first)
+ *   RC_DEC_PAIR=512|1024    decode 2^15 < total <= 2^16 static models with the pair-bucket
+ *                           decoder in workgroups of that size (measurements; slower)
+ *   RC_STREAM_SERVICE=0     per-call stream entry points launch a kernel per call instead of
+ *                           using the stream-service wave
+ *   RC_STREAM_DMA=1         host pipeline (rc_*_host): every transfer by DMA engine copies
+ *   RC_STREAM_DIRECT=0      host pipeline: stage outputs in HBM instead of writing them into
+ *                           mapped host memory from the kernel
+ *   RC_STREAM_BATCH_BYTES=n host pipeline batch size in input bytes (default 2 GiB)
+ *   RC_HIST_HOT=0           rc_histogram without its ballot-counted most frequent symbol */
 typedef struct rc_model rc_model; /* device-resident snapshot of a PModel */
 
 /* ---- context ---- */
@@ -223,7 +237,17 @@ rc_status rc_stream_decode(rc_ctx* ctx, const uint32_t* c_dev, const uint32_t* c
 /* One stream in host memory, synchronous (the host mirrors' Encoder / Decoder).  Only the bytes a
  * call can touch cross PCIe: the encoder's new bytes, the decoder's window
  * [pos, pos + RC_STREAM_MAX_BYTES(n, 0) + 8).  Return RC_E_CHUNK when a flag is set (in
- * *flags_out, and sticky ones in the state).                                                 */
+ * *flags_out, and sticky ones in the state).
+ * Small calls (request and result within 64 KiB) go to the context's stream-service wave: one
+ * workgroup of one wave, launched by the first such call on a stream of its own, holding 64.4 KiB
+ * of one CU's LDS, which polls a mailbox in pinned host memory and leaves 5 ms after its last
+ * request (2 s after its launch at most; the next call launches another).  While it runs it
+ * occupies that CU slot and its hardware queue like any resident kernel.  A call waits for the
+ * wave WITHOUT a time limit while the wave has not started (a wave waiting for a CU behind
+ * long-running kernels is waited for, exactly as a launch would be); once the wave runs, a
+ * call that sees no answer within 10 s returns RC_E_DEVICE and the context's service is off
+ * from then on (later calls take the launch path).  RC_STREAM_SERVICE=0 (below) sends every
+ * call down the launch path.                                                                 */
 rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint32_t* triples,
                                 uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
                                 uint8_t* nbytes, uint32_t finish, uint32_t* flags_out);

@@ -640,16 +640,22 @@ def _canonical_find_index(pmodel):
     the model does not override find_index (pmodel.rs:12), or says its override has those
     semantics (canonical_find_index = True in the class that defines the override)."""
     t = type(pmodel)
-    hit = _CANONICAL.get(t)
-    if hit is None:  # (per class, cached: the MRO scan is ~1 us of every decode call)
+    # (cached per class and per the find_index / canonical_find_index the class resolves to
+    # now: the MRO scan is ~1 us of every decode call, and a class patched after its first
+    # decode gets a new key)
+    key = (t, getattr(t, "find_index", None), getattr(t, "canonical_find_index", None))
+    hit = _CANONICAL.get(key)
+    if hit is None:
         owner = next((k for k in t.__mro__ if "find_index" in vars(k)), None)
         hit = (owner is None or owner is PModel or owner is FreqTable or
                bool(vars(owner).get("canonical_find_index", False)))
-        _CANONICAL[t] = hit
+        if len(_CANONICAL) > 4096:
+            _CANONICAL.clear()
+        _CANONICAL[key] = hit
     return hit
 
 
-_CANONICAL = {}  # PModel class -> whether its find_index keeps FreqTable's semantics
+_CANONICAL = {}  # (class, find_index, flag) -> whether find_index keeps FreqTable's semantics
 
 
 def _find_index_rfreq(st, total):

@@ -39,6 +39,7 @@
 
 #define AWG 64  // one wave per workgroup
 #define TREE_BYTES (255 * 128)
+#define TREE128_BYTES (127 * 128)  // the decoder's tree for models of <= 128 symbols
 #define ROW(j) (((j) - 1) * 128)  // byte offset of node j's row
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -103,30 +104,34 @@ static __device__ __forceinline__ void lwr(u32 a, u32 v) { *(l_u16*)(uintptr_t)a
 
 // ---- the per-lane count tree: node j at t[(j - 1) * 64] ----
 
+// NN: the symbols the tree spans (256; 128 for the decoder of models of <= 128 symbols, whose
+// tree is nodes 1..127 only: node 128, the count of symbols 0..127, is the total itself)
+template <u32 NN = 256>
 static __device__ __forceinline__ void tree_init(uint16_t* t, u32 n) {
-  for (u32 j = 1; j < 256; ++j) {
+  for (u32 j = 1; j < NN; ++j) {
     const u32 lo = j - (j & (0u - j));
     t[(j - 1) * 64] = (uint16_t)(n > lo ? min(n, j) - lo : 0u);
   }
 }
 
 // every c = (c + 1) >> 1: Fenwick -> counts (reverse pass), halve, counts -> Fenwick
+template <u32 NN = 256>
 static __device__ __forceinline__ void tree_halve(uint16_t* t, u32& total) {
-  for (u32 j = 255; j >= 1; --j) {
+  for (u32 j = NN - 1; j >= 1; --j) {
     const u32 k = j + (j & (0u - j));
-    if (k < 256) t[(k - 1) * 64] = (uint16_t)(t[(k - 1) * 64] - t[(j - 1) * 64]);
+    if (k < NN) t[(k - 1) * 64] = (uint16_t)(t[(k - 1) * 64] - t[(j - 1) * 64]);
   }
   u32 sum = 0, nt = 0;
-  for (u32 j = 1; j < 256; ++j) {
+  for (u32 j = 1; j < NN; ++j) {
     const u32 v = t[(j - 1) * 64];
     sum += v;
     nt += (v + 1) >> 1;
     t[(j - 1) * 64] = (uint16_t)((v + 1) >> 1);
   }
-  nt += (total - sum + 1) >> 1;  // c[255] lives only in the total
-  for (u32 j = 1; j < 256; ++j) {
+  nt += (total - sum + 1) >> 1;  // c[NN - 1] lives only in the total
+  for (u32 j = 1; j < NN; ++j) {
     const u32 k = j + (j & (0u - j));
-    if (k < 256) t[(k - 1) * 64] = (uint16_t)(t[(k - 1) * 64] + t[(j - 1) * 64]);
+    if (k < NN) t[(k - 1) * 64] = (uint16_t)(t[(k - 1) * 64] + t[(j - 1) * 64]);
   }
   total = nt;
 }
@@ -691,14 +696,17 @@ struct ADec {
   u32 L0, L1a, L1b, L2a, L2b, L2c, L2d;  // tree levels 0-2 (fixed nodes) of this symbol
 };
 
+template <u32 NN>
 static __device__ __forceinline__ void dec_preread(ADec& d, u32 col) {
-  d.L0 = lrd(col + ROW(128));
+  if (NN == 256) {
+    d.L0 = lrd(col + ROW(128));
+    d.L1b = lrd(col + ROW(192));
+    d.L2c = lrd(col + ROW(160));
+    d.L2d = lrd(col + ROW(224));
+  }
   d.L1a = lrd(col + ROW(64));
-  d.L1b = lrd(col + ROW(192));
   d.L2a = lrd(col + ROW(32));
   d.L2b = lrd(col + ROW(96));
-  d.L2c = lrd(col + ROW(160));
-  d.L2d = lrd(col + ROW(224));
 }
 
 // nb <= 3 code bytes consumed (Decoder::shift_left_buffer, decoder.rs:31-35): a whole dword is
@@ -729,6 +737,9 @@ struct DWalk {
   u32 nv[8], P[8];
 };
 
+// (NN = 128: level 0, node 128, holds the total, so every target q < total turns left there:
+// the walk starts at level 1 and never addresses nodes 129..255)
+template <u32 NN>
 static __device__ __forceinline__ void dec_walk(DWalk& w, const ADec& d, u32 q, u32 col,
                                                 u32 inc) {
   u32 nrem = ~q, e1 = d.total + nrem, P = col;
@@ -743,11 +754,15 @@ static __device__ __forceinline__ void dec_walk(DWalk& w, const ADec& d, u32 q, 
     e1 = min(e1, nd_);                                  \
     P |= mr[l] & ((128u >> (l)) * 128u);                \
   }
-  RC_LEVEL(0, d.L0)
-  RC_LEVEL(1, mselc(mr[0], d.L1b, d.L1a))
-  {
+  if (NN == 256) {
+    RC_LEVEL(0, d.L0)
+    RC_LEVEL(1, mselc(mr[0], d.L1b, d.L1a))
     const u32 t0 = mselc(mr[0], d.L2c, d.L2a), t1 = mselc(mr[0], d.L2d, d.L2b);
     RC_LEVEL(2, mselc(mr[1], t1, t0))
+  } else {
+    mr[0] = 0u;
+    RC_LEVEL(1, d.L1a)
+    RC_LEVEL(2, mselc(mr[1], d.L2b, d.L2a))
   }
   {  // levels 3-5: one 7-node read below P
     const u32 r3 = lrd(P + ROW(16)), r4a = lrd(P + ROW(8)), r4b = lrd(P + ROW(24));
@@ -769,22 +784,23 @@ static __device__ __forceinline__ void dec_walk(DWalk& w, const ADec& d, u32 q, 
   w.c = e1 - nrem;
 }
 
-// c[s] += inc on the walked path
+// c[s] += inc on the walked path (NN = 128: from level 1; node 128 is the total)
+template <u32 NN>
 static __device__ __forceinline__ void dec_update(const DWalk& w) {
 #pragma unroll
-  for (int l = 0; l < 8; ++l) lwr(w.P[l] + ROW(128u >> l), w.nv[l]);
+  for (int l = NN == 256 ? 0 : 1; l < 8; ++l) lwr(w.P[l] + ROW(128u >> l), w.nv[l]);
 }
 
 // Decoder::decode (decoder.rs:38-54) with FreqTable::find_index (sample_impl.rs:27-45) and the
 // model update; returns the symbol.  Wave-uniform call sites only (rare branches inside).
 // at: symbol i is a period end ((i + 1) % period == 0); UNI: at is wave-uniform.
-template <bool UNI, int SM>
+template <bool UNI, int SM, u32 NN>
 static __device__ __forceinline__ u32 dec_step(ADec& d, const ACode& g, u32 col, uint16_t* tcol,
                                                const AdaptParams& p, bool at) {
   // levels 0-2 of the tree (fixed nodes) first: their LDS latency hides behind the hint and
   // range / total.  (Read at the end of the previous symbol and carried instead, they are
   // re-zero-extended by the compiler at the loop latch, which also waits for them there.)
-  dec_preread(d, col);
+  dec_preread<NN>(d, col);
   // (kept here by a scheduling barrier: left to itself the scheduler issues these reads just
   // before the walk needs them, after the hint and the division, and waits for them there)
   __builtin_amdgcn_sched_barrier(0);
@@ -794,7 +810,7 @@ static __device__ __forceinline__ u32 dec_step(ADec& d, const ACode& g, u32 col,
   const u32 q = min(cvt_u32_sat(X * (d.tf * __builtin_amdgcn_rcpf(R))), d.total - 1u);
   const u64 r = div_magic(d.range, d.total, d.M);
   DWalk wk;
-  dec_walk(wk, d, q, col, p.inc);
+  dec_walk<NN>(wk, d, q, col, p.inc);
   u64 A = mul_rs<SM>(r, wk.cum), B = mul_rs<SM>(r, wk.c);
   u64 dx = sub64(d.xlo, d.xhi, A);
   // exact check r*cum <= x < r*(cum+c) as one unsigned test (A + B <= range: a wrapped x - A
@@ -815,20 +831,20 @@ static __device__ __forceinline__ u32 dec_step(ADec& d, const ACode& g, u32 col,
           a += r;
         }
       }
-      dec_walk(wk, d, qe, col, p.inc);
+      dec_walk<NN>(wk, d, qe, col, p.inc);
       A = mul_r(r, wk.cum);
       B = mul_r(r, wk.c);
       dx = sub64(d.xlo, d.xhi, A);
     }
   }
-  dec_update(wk);
+  dec_update<NN>(wk);
   d.total += p.inc;
   d.M = d.Mn;  // magic[total], loaded during this symbol unless a halving changes the total
   if (!UNI || at) {  // the halving check, before the next symbol's tree reads
     const bool h = at && d.total > p.limit;
     if (__builtin_expect(__any((int)h), 0)) {
       if (h) {
-        tree_halve(tcol, d.total);
+        tree_halve<NN>(tcol, d.total);
         d.M = gload64(p.magic + d.total);
       }
     }
@@ -874,25 +890,25 @@ struct DecLane {
 };
 
 // lanes with all their tiles decoded: the tail symbols (per lane) and the flag
-template <int SM>
+template <int SM, u32 NN>
 static __device__ __forceinline__ void dec_lane_end(DecLane& L, const AdaptParams& p, u32 t,
                                                     u32* flags) {
   for (u32 j = 0; j < L.tl; ++j) {
     const u32 i = L.hd + 16 * t + j;
     gstore8(L.op + i,
-            dec_step<false, SM>(L.d, L.g, L.col, L.tcol, p, (i & p.pmask) == p.pmask));
+            dec_step<false, SM, NN>(L.d, L.g, L.col, L.tcol, p, (i & p.pmask) == p.pmask));
   }
   // shift_left_buffer panics once more bytes are needed than the stream holds (decoder.rs:33)
   flags[L.k] = (u64)(L.d.cpos - L.a) > L.clen ? RC_F_TRUNCATED : 0u;
   L.done = true;
 }
 
-template <bool UNI, int SM>
+template <bool UNI, int SM, u32 NN>
 static __device__ __forceinline__ void dec_tiles(DecLane& L, const AdaptParams& p, u32 T,
                                                  u32 hd_u, u32* flags) {
   for (u32 t = 0; t < T; ++t) {
     if (__any((int)(!L.done && t == L.nt))) {
-      if (!L.done && t == L.nt) dec_lane_end<SM>(L, p, t, flags);
+      if (!L.done && t == L.nt) dec_lane_end<SM, NN>(L, p, t, flags);
     }
     const u32 i0 = hd_u + 16 * t;
     const u32 dd = (p.pmask - (L.hd + 16 * t)) & p.pmask;
@@ -905,14 +921,14 @@ static __device__ __forceinline__ void dec_tiles(DecLane& L, const AdaptParams& 
       else  // lanes past their chunk's end halve too: it keeps every total below 2^16, which
             // the magic-table loads rely on
         at = ((u32)j & p.pmask) == dd;
-      o[j >> 2] |= dec_step<UNI, SM>(L.d, L.g, L.col, L.tcol, p, at) << (8 * (j & 3));
+      o[j >> 2] |= dec_step<UNI, SM, NN>(L.d, L.g, L.col, L.tcol, p, at) << (8 * (j & 3));
     }
     if (!L.done) gstore128(L.op + L.hd + 16 * t, (u32x4){o[0], o[1], o[2], o[3]});
   }
-  if (!L.done) dec_lane_end<SM>(L, p, T, flags);
+  if (!L.done) dec_lane_end<SM, NN>(L, p, T, flags);
 }
 
-template <int SM>
+template <int SM, u32 NN>
 __global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_decode_adaptive(
     AdaptParams p, const uint8_t* __restrict__ code, const u64* __restrict__ code_off,
     const u64* __restrict__ code_len, uint8_t* __restrict__ syms_out,
@@ -945,7 +961,7 @@ __global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   // bank (lane pairs sharing a dword conflicted 2-way whenever they read different rows)
   L.col = ((lane & 31u) << 2) | ((lane >> 5) << 1);
   L.tcol = s_tree + (L.col >> 1);
-  tree_init(L.tcol, p.n);
+  tree_init<NN>(L.tcol, p.n);
   ADec& d = L.d;
   d.total = p.n;
   d.tf = (float)p.n;
@@ -982,15 +998,15 @@ __global__ __launch_bounds__(AWG) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   for (u32 j = 0; __any((int)(j < L.hd && !L.done)); ++j) {
     if (j < L.hd && !L.done) {
       gstore8(L.op + j,
-              dec_step<false, SM>(d, L.g, L.col, L.tcol, p, (j & p.pmask) == p.pmask));
+              dec_step<false, SM, NN>(d, L.g, L.col, L.tcol, p, (j & p.pmask) == p.pmask));
     }
   }
   const u32 T = wave_max(L.done ? 0u : L.nt);
   const u32 hmin = wave_min(L.done ? 16u : L.hd), hmax = wave_max(L.done ? 0u : L.hd);
   if (hmin >= hmax)
-    dec_tiles<true, SM>(L, p, T, hmax, flags);
+    dec_tiles<true, SM, NN>(L, p, T, hmax, flags);
   else
-    dec_tiles<false, SM>(L, p, T, 0, flags);
+    dec_tiles<false, SM, NN>(L, p, T, 0, flags);
 }
 
 hipError_t rc_adaptive_encode_launch(hipStream_t stream, const AdaptParams& p,
@@ -1007,22 +1023,18 @@ hipError_t rc_adaptive_decode_launch(hipStream_t stream, const AdaptParams& p,
                                      const uint8_t* code, const u64* code_off,
                                      const u64* code_len, uint8_t* syms_out, const u64* sym_off,
                                      u32 n_chunks, u32* flags) {
-  // Measurements only: RC_ADAPT_DEC_LDS=bytes launches
-  // models of <= 128 symbols with that much LDS per wave (>= the 128 rows of nodes 1..128).
-  // Their nodes 129..255 hold zeros: reads past the allocation return 0 and writes to it are
-  // dropped, so the output stays exact while more waves share a CU.
-  size_t lds = TREE_BYTES;
-  if (const char* e = getenv("RC_ADAPT_DEC_LDS")) {
-    const size_t b = (size_t)strtoul(e, nullptr, 10);
-    if (p.n <= 128 && b >= 128 * 128 && b < TREE_BYTES) lds = b;
-  }
-  // 256-symbol models keep total >= 256 (every count >= 1), so r < 2^56: 24-bit high products
+  // 256-symbol models keep total >= 256 (every count >= 1), so r < 2^56: 24-bit high products.
+  // Models of <= 128 symbols decode with the 127-node tree (16 KiB per wave instead of 32: 8
+  // waves per CU, held by their 176 VGPRs, instead of the 5 the LDS allows with 255 nodes).
+  const dim3 grid((n_chunks + AWG - 1) / AWG), block(AWG);
   if (p.n == 256)
-    hipLaunchKernelGGL(k_decode_adaptive<1>, dim3((n_chunks + AWG - 1) / AWG), dim3(AWG),
-                       TREE_BYTES, stream, p, code, code_off, code_len, syms_out, sym_off,
-                       n_chunks, flags);
+    hipLaunchKernelGGL((k_decode_adaptive<1, 256>), grid, block, TREE_BYTES, stream, p, code,
+                       code_off, code_len, syms_out, sym_off, n_chunks, flags);
+  else if (p.n <= 128)
+    hipLaunchKernelGGL((k_decode_adaptive<0, 128>), grid, block, TREE128_BYTES, stream, p, code,
+                       code_off, code_len, syms_out, sym_off, n_chunks, flags);
   else
-    hipLaunchKernelGGL(k_decode_adaptive<0>, dim3((n_chunks + AWG - 1) / AWG), dim3(AWG), lds,
-                       stream, p, code, code_off, code_len, syms_out, sym_off, n_chunks, flags);
+    hipLaunchKernelGGL((k_decode_adaptive<0, 256>), grid, block, TREE_BYTES, stream, p, code,
+                       code_off, code_len, syms_out, sym_off, n_chunks, flags);
   return hipGetLastError();
 }

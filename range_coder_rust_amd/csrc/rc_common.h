@@ -253,3 +253,22 @@ hipError_t rc_adaptive_decode_launch(hipStream_t stream, const AdaptParams& p,
                                      const uint8_t* code, const u64* code_off,
                                      const u64* code_len, uint8_t* syms_out, const u64* sym_off,
                                      u32 n_chunks, u32* flags);
+
+// Run-time switches (include/range_coder.h, "Environment"): read from the environment ONCE per
+// context, by rc_ctx_create, and carried by the context.  Nothing reads the environment per
+// launch or per call, so a stray variable set later cannot change a live context.  One kill
+// switch per feature; the measurement overrides of earlier rounds are compile-time options of
+// scratch builds (-DRC_PRIO_LAST=x, -DRC_PRIO_RANK, -DRC_PRIO_ROT=k, -DRC_DEC_LDS_PAD=bytes,
+// -DRC_STREAM_COPY_WGS=n).
+struct RcKnobs {
+  bool prio;               // RC_PRIO=off: every wave at priority 0 (oldest-first issue)
+  u32 dec_pair;            // RC_DEC_PAIR=512 | 1024: the pair-bucket decoder (LUT 3) for the
+                           //   models that carry its table (tests and measurements)
+  bool stream_service;     // RC_STREAM_SERVICE=0: the per-call stream API always launches
+  bool stream_dma;         // RC_STREAM_DMA=1: the host pipeline moves everything by DMA
+  bool stream_direct;      // RC_STREAM_DIRECT=0: the host pipeline stages outputs in HBM
+  u64 stream_batch_bytes;  // RC_STREAM_BATCH_BYTES=n: the host pipeline's batch size (0: default)
+  bool hist_hot;           // RC_HIST_HOT=0: the histogram without its ballot-counted hot symbol
+};
+RcKnobs rc_knobs_from_env();                      // rc_kernels.hip (rc_ctx_create only)
+const RcKnobs& rc_ctx_knobs_(const rc_ctx* ctx);  // rc_kernels.hip

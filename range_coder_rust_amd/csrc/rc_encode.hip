@@ -543,15 +543,16 @@ u32 rc_resident_wgs(const void* kernel, int block, size_t lds) {
   return cache[key] = (u32)(per_cu * cus);
 }
 
-hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a_in, int div, int smv,
-                                   const uint8_t* syms, const u64* sym_off, u32 n_chunks,
-                                   uint8_t* out, const u64* out_off, u64* out_len, u32* flags) {
+hipError_t rc_static_encode_launch(hipStream_t stream, const RcKnobs& k, const ModelArgs& a_in,
+                                   int div, int smv, const uint8_t* syms, const u64* sym_off,
+                                   u32 n_chunks, uint8_t* out, const u64* out_off, u64* out_len,
+                                   u32* flags) {
   const dim3 grid((n_chunks + WG - 1) / WG), block(WG);
   ModelArgs a = a_in;
   // (the launch's wave priorities: rc_static.h)
   auto go = [&](auto kern) {
     rc_prio_policy(a, kPrioEncoder, grid.x,
-                   rc_resident_wgs(reinterpret_cast<const void*>(kern), WG, 0));
+                   rc_resident_wgs(reinterpret_cast<const void*>(kern), WG, 0), k);
     hipLaunchKernelGGL(kern, grid, block, 0, stream, a, syms, sym_off, n_chunks, out, out_off,
                        out_len, flags);
   };

@@ -60,7 +60,33 @@ struct rc_ctx {
   hipStream_t own;
   hipStream_t cur;
   uint8_t* inv;  // 64 KiB device scratch for rc_synth_fill's inverse CDF
+  RcKnobs knobs;  // read from the environment once, here (rc_common.h)
 };
+
+// The only place the library reads its environment (tests/test_abi.py checks that no other
+// source calls getenv): once per context, in rc_ctx_create.
+RcKnobs rc_knobs_from_env() {
+  auto str = [](const char* name) -> const char* {
+    const char* e = getenv(name);
+    return e && *e ? e : nullptr;
+  };
+  RcKnobs k;
+  const char* e;
+  k.prio = !((e = str("RC_PRIO")) && !strcmp(e, "off"));
+  k.dec_pair = 0;
+  if ((e = str("RC_DEC_PAIR"))) {
+    const long x = strtol(e, nullptr, 10);
+    k.dec_pair = x == 512 || x == 1024 ? (u32)x : 0u;
+  }
+  k.stream_service = !((e = str("RC_STREAM_SERVICE")) && e[0] == '0');
+  k.stream_dma = (e = str("RC_STREAM_DMA")) && e[0] != '0';
+  k.stream_direct = !((e = str("RC_STREAM_DIRECT")) && e[0] == '0');
+  k.stream_batch_bytes = (e = str("RC_STREAM_BATCH_BYTES")) ? strtoull(e, nullptr, 0) : 0ull;
+  k.hist_hot = !((e = str("RC_HIST_HOT")) && e[0] == '0');
+  return k;
+}
+
+const RcKnobs& rc_ctx_knobs_(const rc_ctx* ctx) { return ctx->knobs; }
 
 struct rc_model {
   int kind;  // 0 static, 1 adaptive
@@ -196,6 +222,7 @@ rc_status rc_ctx_create(int device, rc_ctx** out) {
   if (!g.ok) return RC_E_DEVICE;
   rc_ctx* c = new rc_ctx;
   c->device = device;
+  c->knobs = rc_knobs_from_env();
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return RC_E_DEVICE;
@@ -501,8 +528,8 @@ rc_status rc_encode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   }
   const bool sm = m->args.total >= 256 && m->args.total <= 65536;
   const int smv = sm ? (m->complete ? 2 : 1) : 0;
-  const hipError_t e = rc_static_encode_launch(ctx->cur, m->args, m->div, smv, syms, sym_off,
-                                               n_chunks, out, out_off, out_len, flags);
+  const hipError_t e = rc_static_encode_launch(ctx->cur, ctx->knobs, m->args, m->div, smv, syms,
+                                               sym_off, n_chunks, out, out_off, out_len, flags);
   return e == hipSuccess ? RC_OK : device_error(e, "encode launch");
 }
 
@@ -523,9 +550,9 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   const bool sm = m->args.total >= 256 && m->args.total <= 65536;
   const hipError_t e =
       m->div == DIV_POW2
-          ? rc_static_decode_launch_pow2(ctx->cur, m->args, sm, code, code_off, code_len,
+          ? rc_static_decode_launch_pow2(ctx->cur, ctx->knobs, m->args, sm, code, code_off, code_len,
                                          syms_out, sym_off, n_chunks, flags)
-          : rc_static_decode_launch_magic(ctx->cur, m->args, sm, code, code_off, code_len,
+          : rc_static_decode_launch_magic(ctx->cur, ctx->knobs, m->args, sm, code, code_off, code_len,
                                           syms_out, sym_off, n_chunks, flags);
   return e == hipSuccess ? RC_OK : device_error(e, "decode launch");
 }

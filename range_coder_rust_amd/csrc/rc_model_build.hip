@@ -223,10 +223,10 @@ rc_status rc_histogram(rc_ctx* ctx, const uint8_t* syms, const uint64_t* sym_off
     return RC_E_DEVICE;
   // 16 KiB LDS per workgroup: 8 workgroups (32 waves) per CU
   const u32 grid = std::min<u32>(n_chunks, (u32)cus * 8);
-  // RC_HIST_HOT=0 turns the ballot-counted hot symbol off (measurements)
-  const char* hot = getenv("RC_HIST_HOT");
+  // RC_HIST_HOT=0 (in the environment of rc_ctx_create) turns the ballot-counted hot symbol
+  // off (measurements)
   hipLaunchKernelGGL(k_histogram, dim3(grid), dim3(256), 0, s, syms, sym_off, n_chunks,
-                     chunk_hist, hist, (u32)!(hot && *hot == '0'));
+                     chunk_hist, hist, (u32)rc_ctx_knobs_(ctx).hist_hot);
   return hipGetLastError() == hipSuccess ? RC_OK : RC_E_DEVICE;
 }
 

@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <memory>
 #include <mutex>
@@ -528,20 +529,32 @@ struct Svc {
 std::mutex g_svc_mu;
 std::unordered_map<const rc_ctx*, std::shared_ptr<Svc>> g_svcs;
 // at process exit, tell any running wave to leave (no HIP calls: the runtime may be going too;
-// a wave leaves within one poll, and by SVC_IDLE_MS in any case)
+// a wave leaves within one poll, and by SVC_IDLE_MS in any case).  The box is written only under
+// its service's lock, which a call that times out holds while it frees the box; a service whose
+// lock another thread holds is skipped (its wave leaves by itself after SVC_IDLE_MS).
 struct SvcAtExit {
   ~SvcAtExit() {
     std::lock_guard<std::mutex> g(g_svc_mu);
-    for (auto& kv : g_svcs)
-      if (kv.second && kv.second->box) __atomic_store_n(&kv.second->box->stop, 1u, __ATOMIC_RELEASE);
+    for (auto& kv : g_svcs) {
+      if (!kv.second) continue;
+      std::unique_lock<std::mutex> lk(kv.second->mu, std::try_to_lock);
+      if (lk.owns_lock() && kv.second->box)
+        __atomic_store_n(&kv.second->box->stop, 1u, __ATOMIC_RELEASE);
+    }
   }
 } g_svc_at_exit;
 
-// RC_STREAM_SERVICE=0 sends every call down the launch path (read at every call, so tests can
-// switch it between calls; a getenv is ~0.1 us)
-bool svc_enabled() {
-  const char* e = getenv("RC_STREAM_SERVICE");
-  return !(e && e[0] == '0');
+// RC_STREAM_SERVICE=0 in the environment of rc_ctx_create sends every call of that context down
+// the launch path (RcKnobs, rc_common.h)
+bool svc_enabled(const rc_ctx* ctx) { return rc_ctx_knobs_(ctx).stream_service; }
+
+// Test hook (tests/test_gpu_stream.py, not in include/range_coder.h): the wave's idle time in
+// 10-ns ticks for the waves launched from now on (0: SVC_IDLE_MS), so a test can make waves
+// leave at the moment requests are published.
+std::atomic<u64> g_svc_idle_ticks{0};
+u64 idle_ticks() {
+  const u64 t = g_svc_idle_ticks.load(std::memory_order_relaxed);
+  return t ? t : (u64)SVC_IDLE_MS * 100000ull;
 }
 
 std::shared_ptr<Svc> svc_get(const rc_ctx* ctx) {
@@ -622,7 +635,7 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, int dev, Fill fill, rc_status* err) {
       Dev g(dev);
       ++sv->epoch;
       hipLaunchKernelGGL(k_stream_service, dim3(1), dim3(RWG), 0, sv->stream, sv->dbox_host,
-                         sv->epoch, (u64)SVC_IDLE_MS * 100000ull,
+                         sv->epoch, idle_ticks(),
                          (u64)SVC_LIFE_MS * 100000ull);
       if (hipGetLastError() != hipSuccess) {
         sv->broken = true;
@@ -643,8 +656,9 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, int dev, Fill fill, rc_status* err) {
         *err = RC_E_DEVICE;
         return true;
       }
-      if (hipStreamQuery(sv->stream) != hipSuccess &&
-          hipStreamQuery(sv->stream) != hipErrorNotReady) {
+      // (one query: a wave that leaves between two queries would read as a fault)
+      const hipError_t q = hipStreamQuery(sv->stream);
+      if (q != hipSuccess && q != hipErrorNotReady) {
         sv->broken = true;
         *err = RC_E_DEVICE;
         return true;
@@ -712,7 +726,7 @@ rc_status rc_stream_encode_host(rc_ctx* ctx, rc_stream_state* state, const uint3
   const size_t o_off = 64, o_len = o_off + 32, o_fl = o_len + 16, o_tr = o_fl + 16;
   const size_t o_nb = o_tr + ((12 * n + 15) & ~15ull), o_out = o_nb + ((n + 15) & ~15ull);
   const size_t tail = (o_out + need - o_nb + 15) & ~15ull;
-  if (svc_enabled() && o_nb + tail <= SVC_BLOCK) {  // a small call: through the stream service
+  if (svc_enabled(ctx) && o_nb + tail <= SVC_BLOCK) {  // a small call: through the stream service
     auto sv = svc_get(ctx);
     std::lock_guard<std::mutex> slk(sv->mu);
     rc_status err = RC_OK;
@@ -817,7 +831,7 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
   const size_t o_off = 64, o_fl = o_off + 32, o_c = o_fl + 16, o_cum = o_c + 1024;
   const size_t o_win = o_cum + 1024, o_sym = o_win + ((wlen + 15) & ~15ull);
   const size_t tail = (n + 15) & ~15ull;
-  if (svc_enabled() && o_sym + tail <= SVC_BLOCK) {  // a small call: through the stream service
+  if (svc_enabled(ctx) && o_sym + tail <= SVC_BLOCK) {  // a small call: through the stream service
     auto sv = svc_get(ctx);
     std::lock_guard<std::mutex> slk(sv->mu);
     rc_status err = RC_OK;
@@ -898,6 +912,11 @@ rc_status rc_stream_decode_host(rc_ctx* ctx, const uint32_t* c, const uint32_t* 
 // timings since the last call, then reset: out[0] calls; out[1..3] the wave's 10-ns ticks summed
 // from seeing a request to its block in LDS, to the body done, to the results written back;
 // out[4] the host's wait from publishing the request to seeing its ack, in ns, summed.
+rc_status rc_svc_set_idle_ticks_(uint64_t ticks) {
+  g_svc_idle_ticks.store(ticks, std::memory_order_relaxed);
+  return RC_OK;
+}
+
 rc_status rc_svc_probe_(rc_ctx* ctx, uint64_t* out) {
   if (!ctx || !out) return RC_E_ARG;
   auto sv = svc_get(ctx);

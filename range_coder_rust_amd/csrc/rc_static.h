@@ -115,9 +115,10 @@ struct ModelArgs {
 //    turn: issue goes round-robin at 2^k x 10 ns granularity instead of oldest-first, and waves
 //    that started together finish together (the two waves of one 512-lane workgroup on a SIMD,
 //    whose slots are released together; rounds that divide the grid evenly).
-// Control (read at every launch): RC_PRIO=off; RC_PRIO_LAST=x (the last x rounds at priority
-// 1, x may be fractional), RC_PRIO_RANK=1 (the last three rounds at priorities 1, 2, 3),
-// RC_PRIO_ROT=k (rotation every 2^k ticks, 0 off); unset: the kernel's default.
+// Control: RC_PRIO=off in the environment of rc_ctx_create (RcKnobs) turns priorities off;
+// scratch builds override every kernel's default at compile time: -DRC_PRIO_LAST=x (the last x
+// rounds at priority 1, x may be fractional), -DRC_PRIO_RANK (the last three rounds at 1, 2, 3),
+// -DRC_PRIO_ROT=k (rotation every 2^k ticks, 0 off).
 struct PrioPolicy {
   float last_rounds;  // > 0: the last last_rounds x R workgroups at priority 1
   bool rank;          // the last three rounds at 1, 2, 3
@@ -136,17 +137,22 @@ static constexpr u32 kRotAuto = 0xFFu;
 static constexpr PrioPolicy kPrioEncoder{0.0f, false, 12u};
 static constexpr PrioPolicy kPrioDecoder{1.0f, false, 0u};
 static constexpr PrioPolicy kPrioDecoder512{0.0f, false, kRotAuto};
-static inline void rc_prio_policy(ModelArgs& a, PrioPolicy dflt, u32 grid, u32 resident) {
+static inline void rc_prio_policy(ModelArgs& a, PrioPolicy dflt, u32 grid, u32 resident,
+                                  const RcKnobs& k) {
   a.prio_base = ~0u;
   a.prio_step = 1u << 31;
   a.prio_rot = 0;
-  const char* off = getenv("RC_PRIO");
-  if (off && !strcmp(off, "off")) return;
+  if (!k.prio) return;
   PrioPolicy p = dflt;
-  const char* e;
-  if ((e = getenv("RC_PRIO_LAST")) && *e) p = {(float)atof(e), false, 0u};
-  if ((e = getenv("RC_PRIO_RANK")) && *e) p = {0.0f, atoi(e) != 0, 0u};
-  if ((e = getenv("RC_PRIO_ROT")) && *e) p.rot = (u32)strtoul(e, nullptr, 10);
+#ifdef RC_PRIO_LAST
+  p = {(float)(RC_PRIO_LAST), false, 0u};
+#endif
+#ifdef RC_PRIO_RANK
+  p = {0.0f, true, 0u};
+#endif
+#ifdef RC_PRIO_ROT
+  p.rot = (u32)(RC_PRIO_ROT);
+#endif
   if (p.rot == kRotAuto) p.rot = resident && grid > resident ? 12u : 10u;
   a.prio_rot = p.rot;
   if (!resident) return;
@@ -276,17 +282,20 @@ static __device__ __forceinline__ u32 ffbh(u32 v) {
 }
 
 // launchers (one translation unit each, so the variants compile in parallel)
-hipError_t rc_static_encode_launch(hipStream_t stream, const ModelArgs& a, int div, int smv,
-                                   const uint8_t* syms, const u64* sym_off, u32 n_chunks,
-                                   uint8_t* out, const u64* out_off, u64* out_len, u32* flags);
+hipError_t rc_static_encode_launch(hipStream_t stream, const RcKnobs& k, const ModelArgs& a,
+                                   int div, int smv, const uint8_t* syms, const u64* sym_off,
+                                   u32 n_chunks, uint8_t* out, const u64* out_off, u64* out_len,
+                                   u32* flags);
 // dynamic LDS bytes of k_decode_static for a model (lut3: the pair-bucket variant, wgs lanes
 // per workgroup)
 size_t rc_static_decode_lds(const ModelArgs& a, int lut3, u32 wgs);
-hipError_t rc_static_decode_launch_pow2(hipStream_t stream, const ModelArgs& a, int sm,
+hipError_t rc_static_decode_launch_pow2(hipStream_t stream, const RcKnobs& k, const ModelArgs& a,
+                                        int sm,
                                         const uint8_t* code, const u64* code_off,
                                         const u64* code_len, uint8_t* syms_out,
                                         const u64* sym_off, u32 n_chunks, u32* flags);
-hipError_t rc_static_decode_launch_magic(hipStream_t stream, const ModelArgs& a, int sm,
+hipError_t rc_static_decode_launch_magic(hipStream_t stream, const RcKnobs& k, const ModelArgs& a,
+                                         int sm,
                                          const uint8_t* code, const u64* code_off,
                                          const u64* code_len, uint8_t* syms_out,
                                          const u64* sym_off, u32 n_chunks, u32* flags);

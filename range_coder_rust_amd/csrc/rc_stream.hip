@@ -47,8 +47,10 @@
 #define RC_STREAM_BATCH_BYTES (2ull << 30)
 #define RC_STEP_COPIES 4  // copies per launch of k_pcie_copy (a batch's output: data, lengths,
                           // flags)
+#ifndef RC_COPY_WGS
 #define RC_COPY_WGS 256   // workgroups per bulk copy (tools/pcie_kernel_probe.hip: 256 keeps
                           // 46.7 GB/s each way with both directions at once; 2048 drops to 33)
+#endif
 
 struct rc_ctx;
 struct rc_model;
@@ -97,18 +99,6 @@ const uint8_t* mapped(const void* host) {
     return nullptr;
   }
   return (const uint8_t*)d;
-}
-
-bool use_dma() {
-  const char* e = getenv("RC_STREAM_DMA");
-  return e && *e && *e != '0';
-}
-
-// outputs written by the batch kernel straight into the mapped host buffer (default), or
-// staged in HBM and moved by k_pcie_copy (RC_STREAM_DIRECT=0)
-bool use_direct() {
-  const char* e = getenv("RC_STREAM_DIRECT");
-  return !(e && *e == '0');
 }
 
 struct CopyArgs {
@@ -185,11 +175,7 @@ bool copy_step(const std::vector<Copy>& cs, hipStream_t s) {
     ++k;
   }
   if (k == 0) return true;
-  static const u64 wgs = [] {
-    const char* e = getenv("RC_STREAM_COPY_WGS");
-    return e && atoi(e) > 0 ? (u64)atoi(e) : (u64)RC_COPY_WGS;
-  }();
-  const unsigned gx = (unsigned)std::min<u64>(wgs, (nmax + 16383) / 16384);
+  const unsigned gx = (unsigned)std::min<u64>(RC_COPY_WGS, (nmax + 16383) / 16384);
   hipLaunchKernelGGL(k_pcie_copy, dim3(gx, k), dim3(256), 0, s, a);
   return hipGetLastError() == hipSuccess;
 }
@@ -331,24 +317,16 @@ struct PipeLease {
   }
 };
 
-// batch size: RC_STREAM_BATCH_BYTES, or the environment variable of that name (tests use small
-// batches to run many of them)
-u64 batch_bytes() {
-  const char* e = getenv("RC_STREAM_BATCH_BYTES");
-  const u64 v = e ? strtoull(e, nullptr, 0) : 0;
-  return v ? v : RC_STREAM_BATCH_BYTES;
-}
-
-// cut [0, n) into batches of about batch_bytes() of input (>= 1 chunk each; the first two
-// of 1/4 and 1/2 of that).  A chunk for which alone(k) holds (one the kernel flags
+// cut [0, n) into batches of about `bytes` of input (>= 1 chunk each; the first two of 1/4
+// and 1/2 of that).  A chunk for which alone(k) holds (one the kernel flags
 // RC_F_TOO_LONG without reading or writing it) is a batch of its own, so no batch's input or
 // output range spans its bytes.
 template <class InRange, class OutRange, class Alone>
-std::vector<Batch> plan(u32 n, InRange in_range, OutRange out_range, Alone alone) {
+std::vector<Batch> plan(u64 bytes, u32 n, InRange in_range, OutRange out_range, Alone alone) {
   std::vector<Batch> b;
   u32 k = 0;
   while (k < n) {
-    const u64 cap = batch_bytes() >> (b.size() < 2 ? 2 - b.size() : 0);
+    const u64 cap = bytes >> (b.size() < 2 ? 2 - b.size() : 0);
     Batch x{};
     x.k0 = k;
     u64 lo, hi, olo, ohi;
@@ -419,7 +397,9 @@ rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   DevSet g(dev);
   // a chunk the kernel flags RC_F_TOO_LONG (never read nor written) is staged as empty
   auto too_long = [&](u32 k) { return sym_off[k + 1] - sym_off[k] > RC_MAX_CHUNK_SYMBOLS; };
+  const RcKnobs& kn = rc_ctx_knobs_(ctx);
   std::vector<Batch> bs = plan(
+      kn.stream_batch_bytes ? kn.stream_batch_bytes : (u64)RC_STREAM_BATCH_BYTES,
       n_chunks,
       [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = too_long(k) ? a : sym_off[k + 1]; },
       [&](u32 k, u64& a, u64& b) { a = out_off[k], b = too_long(k) ? a : out_off[k + 1]; },
@@ -435,13 +415,13 @@ rc_status rc_encode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   // (the pins outlive the lease, whose destructor drains the streams on every return path)
   Pin pin_in(syms + sym_off[0], sym_off[n_chunks] - sym_off[0]);
   Pin pin_out(out + out_off[0], out_off[n_chunks] - out_off[0]);
-  const bool dma = use_dma();
+  const bool dma = kn.stream_dma;
   const uint8_t* const m_out = dma ? nullptr : mapped(out + out_off[0]);
   PipeLease lease{ctx, pipe_acquire(ctx, dev, in_max, out_max, kmax, n_chunks, n_off)};
   if (!lease.p) return RC_E_DEVICE;
   Pipe& p = *lease.p;
   const uint8_t* const m_len = m_out ? mapped(p.hlen) : nullptr;
-  const bool direct = m_out && use_direct();
+  const bool direct = m_out && kn.stream_direct;
   const uint8_t* const m_fl = m_out ? mapped(p.hfl) : nullptr;
   // the caller's stream must not run ahead into our buffers, nor we into its pending work
   (void)hipStreamSynchronize(s0);
@@ -500,7 +480,9 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
     if (sym_off[k + 1] < sym_off[k]) return RC_E_ARG;
   DevSet g(dev);
   auto too_long = [&](u32 k) { return sym_off[k + 1] - sym_off[k] > RC_MAX_CHUNK_SYMBOLS; };
+  const RcKnobs& kn = rc_ctx_knobs_(ctx);
   std::vector<Batch> bs = plan(
+      kn.stream_batch_bytes ? kn.stream_batch_bytes : (u64)RC_STREAM_BATCH_BYTES,
       n_chunks,
       [&](u32 k, u64& a, u64& b) { a = code_off[k], b = too_long(k) ? a : a + code_len[k]; },
       [&](u32 k, u64& a, u64& b) { a = sym_off[k], b = too_long(k) ? a : sym_off[k + 1]; },
@@ -518,13 +500,13 @@ rc_status rc_decode_host(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   }
   Pin pin_in(code + cmin, cmax - cmin);
   Pin pin_out(syms_out + sym_off[0], sym_off[n_chunks] - sym_off[0]);
-  const bool dma = use_dma();
+  const bool dma = kn.stream_dma;
   const uint8_t* const m_out = dma ? nullptr : mapped(syms_out + sym_off[0]);
   PipeLease lease{ctx, pipe_acquire(ctx, dev, in_max, out_max, kmax, n_chunks, n_off)};
   if (!lease.p) return RC_E_DEVICE;
   Pipe& p = *lease.p;
   const uint8_t* const m_fl = m_out ? mapped(p.hfl) : nullptr;
-  const bool direct = m_out && use_direct();
+  const bool direct = m_out && kn.stream_direct;
   (void)hipStreamSynchronize(s0);
   size_t o = 0;
   auto in = [&](size_t t, int i, std::vector<Copy>& cs) {

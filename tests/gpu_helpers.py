@@ -1,7 +1,5 @@
 """Helpers shared by the GPU parity tests: device upload and encode/decode through the C ABI
 with ragged, optionally misaligned chunk layouts and sentinel checks around the slots."""
-import contextlib
-
 import numpy as np
 import torch
 
@@ -67,17 +65,3 @@ def run_decode(model, codes, counts, misalign=False, seed=0, code_lens=None):
     s = syms.cpu().numpy()
     return [s[sym_off[k]:sym_off[k + 1]] for k in range(n)], flags.cpu().numpy()
 
-
-@contextlib.contextmanager
-def knob_context(monkeypatch, **env):
-    """A fresh context created with `env` set: the library reads its run-time switches
-    (RC_DEC_PAIR, RC_DEC_ILP, RC_STREAM_*, RC_PRIO, RC_HIST_HOT) once per context, when it is
-    created (include/range_coder.h, rc_ctx_create)."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, str(v))
-    c = rc.Context(0)
-    try:
-        yield c
-    finally:
-        torch.cuda.synchronize()
-        c.close()

@@ -102,3 +102,19 @@ def test_which_models_keep_the_decode_ahead_path():
         pass
 
     assert api._canonical_find_index(P())
+
+
+def test_canonical_check_follows_a_class_patched_after_first_decode():
+    """the per-class cache is keyed by what the class resolves now, so setting
+    find_index (or the flag) on a class after its first check is seen."""
+    class Q(rc.FreqTable):
+        pass
+
+    assert api._canonical_find_index(Q(4))
+    Q.find_index = lambda self, decoder: 0
+    assert not api._canonical_find_index(Q(4))
+    Q.canonical_find_index = True
+    assert api._canonical_find_index(Q(4))
+    del Q.find_index
+    del Q.canonical_find_index
+    assert api._canonical_find_index(Q(4))

@@ -22,8 +22,9 @@ def ctx():
 
 
 @pytest.fixture
-def small_batches(monkeypatch):
-    monkeypatch.setenv("RC_STREAM_BATCH_BYTES", "20000")
+def small_batches(knob_ctx):
+    """A context whose host pipeline cuts 20,000-byte batches (many batches per call)."""
+    return knob_ctx(RC_STREAM_BATCH_BYTES=20000)
 
 
 def layout(rng, n, lo, hi, gap=False):
@@ -41,7 +42,7 @@ def layout(rng, n, lo, hi, gap=False):
 def test_encode_host_matches_oracle(ctx, small_batches, gap):
     rng = np.random.default_rng(3 + gap)
     c, cum, total = synth.zipf_table()
-    m = rc.StaticModel(c, cum, total)
+    m = rc.StaticModel(c, cum, total, ctx=small_batches)
     n = 120
     lens, soff = layout(rng, n, 0, 3000, gap)
     syms = rng.choice(256, int(soff[-1]), p=np.asarray(c, float) / np.sum(c)).astype(np.uint8)
@@ -64,7 +65,7 @@ def test_encode_host_matches_oracle(ctx, small_batches, gap):
 
 
 def test_flags_returned(ctx, small_batches):
-    m = rc.StaticModel([1, 5, 2, 0, 2, 2, 1, 1, 1, 1])
+    m = rc.StaticModel([1, 5, 2, 0, 2, 2, 1, 1, 1, 1], ctx=small_batches)
     syms = np.array([1, 2, 3, 1, 2, 12], np.uint8)
     soff = np.array([0, 3, 5, 6])
     ooff = np.array([0, 64, 128, 192])
@@ -106,13 +107,12 @@ def test_large_round_trip(ctx, pinned):
     assert (fd == 0).all() and (dec == syms).all()
 
 
-def test_cached_pipeline_across_shapes(monkeypatch):
+def test_cached_pipeline_across_shapes(knob_ctx):
     """The host pipeline is kept with its context: a small call, a larger one (the pipe grows),
     a smaller one again (reused), then rc_ctx_destroy frees it; every call byte-exact."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    monkeypatch.setenv("RC_STREAM_BATCH_BYTES", "50000")
-    own = rc.Context(0)
+    own = knob_ctx(RC_STREAM_BATCH_BYTES=50000)
     try:
         c, cum, total = synth.zipf_table()
         m = rc.StaticModel(c, cum, total, ctx=own)
@@ -162,17 +162,15 @@ def test_host_multi_device_list_equals_single(ctx):
 
 
 @pytest.mark.parametrize("dma,direct", [("0", "1"), ("0", "0"), ("1", "1")])
-def test_output_copy_paths_on_offset_pinned_buffers(ctx, monkeypatch, dma, direct):
+def test_output_copy_paths_on_offset_pinned_buffers(ctx, knob_ctx, dma, direct):
     """Outputs written by the coder straight into mapped host memory (default), staged and moved
     by the copy kernel (RC_STREAM_DIRECT=0), or moved by DMA (RC_STREAM_DMA=1): all byte-exact,
     on pinned buffers used at odd offsets (interior mapped pointers, staging displaced to the
     host address mod 64) across several batches."""
-    monkeypatch.setenv("RC_STREAM_DMA", dma)
-    monkeypatch.setenv("RC_STREAM_DIRECT", direct)
-    monkeypatch.setenv("RC_STREAM_BATCH_BYTES", "300000")
+    kc = knob_ctx(RC_STREAM_DMA=dma, RC_STREAM_DIRECT=direct, RC_STREAM_BATCH_BYTES=300000)
     rng = np.random.default_rng(29)
     c, cum, total = synth.zipf_table()
-    m = rc.StaticModel(c, cum, total)
+    m = rc.StaticModel(c, cum, total, ctx=kc)
     n = 96
     lens, soff = layout(rng, n, 0, 20000, gap=True)
     nsym = int(soff[-1])
@@ -195,12 +193,11 @@ def test_output_copy_paths_on_offset_pinned_buffers(ctx, monkeypatch, dma, direc
     assert (fd == 0).all() and (dec == syms[soff[0]: soff[-1]]).all()
 
 
-def test_adaptive_model_through_host_path(ctx, monkeypatch):
+def test_adaptive_model_through_host_path(ctx, knob_ctx):
     """The host pipeline with the adaptive (C4) model: ragged chunks across several batches,
     every stream byte-exact vs the adaptive oracle and the round trip exact."""
-    monkeypatch.setenv("RC_STREAM_BATCH_BYTES", "40000")
     rng = np.random.default_rng(41)
-    m = rc.AdaptiveModel(256, 32, 57343, 256)
+    m = rc.AdaptiveModel(256, 32, 57343, 256, ctx=knob_ctx(RC_STREAM_BATCH_BYTES=40000))
     n = 40
     lens, soff = layout(rng, n, 0, 6000)
     w = 1.0 / np.arange(1, 257) ** 1.2

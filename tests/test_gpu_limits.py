@@ -109,11 +109,11 @@ def test_host_stream_too_long_chunk(ctx):
 
 
 @pytest.mark.parametrize("direct", ["1", "0"])
-def test_host_stream_too_long_chunk_mid_batch(ctx, monkeypatch, direct):
+def test_host_stream_too_long_chunk_mid_batch(ctx, knob_ctx, direct):
     """A too-long chunk between in-limit chunks of one batch: its input is not staged and its
     output slot is not overwritten, on the direct (mapped) and staged output paths."""
-    monkeypatch.setenv("RC_STREAM_DIRECT", direct)
-    m = _models(ctx)["zipf"]
+    zc, zcum, zt = synth.zipf_table()
+    m = rc.StaticModel(zc, zcum, zt, ctx=knob_ctx(RC_STREAM_DIRECT=direct))
     rng = np.random.default_rng(4)
     n_big = MAX + 1
     syms = np.zeros(200 + n_big + 300, np.uint8)

@@ -506,17 +506,11 @@ def _pair_models(rng):
     return out
 
 
-@pytest.mark.parametrize("pair", ["512", "1024", "0"])
-def test_pair_bucket_decoder_vs_oracle(ctx, monkeypatch, pair):
-    """k_decode_static LUT 3 (both candidates of a bucket in one 16-B LDS entry) at both
-    workgroup sizes, and the bucket decoder it replaces at low occupancy (RC_DEC_PAIR=0), on the
-    same streams: decoded symbols against the oracle's, ragged and misaligned chunks; garbage
-    streams decode like the reference's find_index, flags included."""
-    monkeypatch.setenv("RC_DEC_PAIR", pair)
+def _pair_decoder_cases(kc):
     rng = np.random.default_rng(77)
     for mi, (c, total) in enumerate(_pair_models(rng)):
         cum = cum_of(c)
-        m = rc.StaticModel(c, cum, total)
+        m = rc.StaticModel(c, cum, total, ctx=kc)
         nz = np.nonzero(c)[0]
         p = c[nz] / c[nz].sum()
         lens = list(rng.choice([0, 1, 15, 16, 17, 64, 65, 257, 1000, 4099], 96))
@@ -534,3 +528,12 @@ def test_pair_bucket_decoder_vs_oracle(ctx, monkeypatch, pair):
             assert fd[k] == f, (mi, k, fd[k], f)
             if f == 0:
                 assert (dec[k] == d).all(), (mi, k)
+
+
+@pytest.mark.parametrize("pair", ["512", "1024", "0"])
+def test_pair_bucket_decoder_vs_oracle(ctx, knob_ctx, pair):
+    """k_decode_static LUT 3 (both candidates of a bucket in one 16-B LDS entry) at both
+    workgroup sizes, and the bucket decoder it replaces at low occupancy (RC_DEC_PAIR=0), on the
+    same streams: decoded symbols against the oracle's, ragged and misaligned chunks; garbage
+    streams decode like the reference's find_index, flags included."""
+    _pair_decoder_cases(knob_ctx(RC_DEC_PAIR=pair))

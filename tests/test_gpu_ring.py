@@ -65,12 +65,11 @@ def _decode_at(m, chunks, head, reps=1):
 
 @pytest.mark.parametrize("pair", ["512", "1024", "0"])
 @pytest.mark.parametrize("head", [0, 5, 48])
-def test_ring_fixtures_decode(ctx, ring_fx, monkeypatch, pair, head):
-    monkeypatch.setenv("RC_DEC_PAIR", pair)
+def test_ring_fixtures_decode(ctx, ring_fx, knob_ctx, pair, head):
     c = np.array(ring_fx["c"], np.uint32)
     cum = np.array(ring_fx["cum"], np.uint32)
-    m = rc.StaticModel(c, cum, ring_fx["total"])
     chunks = ring_fx["chunks"]
+    m = rc.StaticModel(c, cum, ring_fx["total"], ctx=knob_ctx(RC_DEC_PAIR=pair))
     s, sym_off, flags = _decode_at(m, chunks, head)
     assert (flags == 0).all(), flags
     assert (s[:head] == 0xEE).all() and (s[sym_off[-1]:] == 0xEE).all()
@@ -79,16 +78,15 @@ def test_ring_fixtures_decode(ctx, ring_fx, monkeypatch, pair, head):
         assert (got == np.array(ch["symbols"], np.uint8)).all(), (pair, head, k)
 
 
-def test_ring_fixtures_full_waves(ctx, ring_fx, monkeypatch):
+def test_ring_fixtures_full_waves(ctx, ring_fx, knob_ctx):
     """Every fixture in many lanes at once (whole workgroups of the bucket decoder, LUT 4: the
     fixtures' model, total 2^16, has 2^12 buckets and so runs 512-lane workgroups, the variant
     2^20-chunk launches of this model take), against the oracle's decode."""
-    monkeypatch.setenv("RC_DEC_PAIR", "0")
     c = np.array(ring_fx["c"], np.uint32)
     cum = np.array(ring_fx["cum"], np.uint32)
     total = ring_fx["total"]
-    m = rc.StaticModel(c, cum, total)
     chunks = ring_fx["chunks"]
+    m = rc.StaticModel(c, cum, total, ctx=knob_ctx(RC_DEC_PAIR="0"))
     s, sym_off, flags = _decode_at(m, chunks, 0, reps=64)
     assert (flags == 0).all()
     for k in range(len(flags)):

@@ -3,6 +3,7 @@ oracles: Encoder / Decoder with a PModel the caller changes between calls, encod
 counts, peek_code, range_coder / data, Decoder without a symbol count, errors at the exact
 call; and the batch device entry points against orc_stream_* with random (even inconsistent)
 tables, garbage streams, split calls and 64-bit stream positions."""
+import ctypes
 import random
 
 import numpy as np
@@ -13,6 +14,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 import range_coder_rust_amd as rc  # noqa: E402
+from range_coder_rust_amd import synth  # noqa: E402
 from oracle import cpu, ref_literal as R  # noqa: E402
 from gpu_helpers import dev  # noqa: E402
 
@@ -560,11 +562,11 @@ def _adaptive_round_trip(ctx_, n=1500, seed=11):
 
 
 @pytest.mark.parametrize("service", ["1", "0"])
-def test_service_and_launch_paths_vs_reference(ctx, monkeypatch, service):
+def test_service_and_launch_paths_vs_reference(ctx, knob_ctx, service):
     """The same caller-adaptive round trip through the service (default) and through the
-    launch path (RC_STREAM_SERVICE=0), against ref_literal's bytes and encode() counts."""
-    monkeypatch.setenv("RC_STREAM_SERVICE", service)
-    syms, code, rets, out = _adaptive_round_trip(ctx)
+    launch path (a context created with RC_STREAM_SERVICE=0), against ref_literal's bytes and
+    encode() counts."""
+    syms, code, rets, out = _adaptive_round_trip(knob_ctx(RC_STREAM_SERVICE=service))
     assert code == R.encode_adaptive_stream(256, 32, 4000, 64, syms)
     ref = R.Encoder()
     ref_m = R.AdaptiveModel(256, 32, 4000, 64)
@@ -576,12 +578,11 @@ def test_service_and_launch_paths_vs_reference(ctx, monkeypatch, service):
     assert out == syms
 
 
-def test_service_restarts_after_idle_and_stops_on_destroy(ctx, monkeypatch):
+def test_service_restarts_after_idle_and_stops_on_destroy(ctx):
     """The wave leaves after its idle time; the next call starts a new one.  rc_ctx_destroy
     with a wave running returns promptly, and torch.cuda.synchronize() is not held up for
     longer than the idle time."""
     import time
-    monkeypatch.setenv("RC_STREAM_SERVICE", "1")
     c2 = rc.Context(0)
     try:
         sd = _sample_table()
@@ -603,3 +604,89 @@ def test_service_restarts_after_idle_and_stops_on_destroy(ctx, monkeypatch):
         t0 = time.perf_counter()
         c2.close()
         assert time.perf_counter() - t0 < 1.0
+
+
+def _set_idle_ticks(ticks):
+    L = rc._native.load()
+    L.rc_svc_set_idle_ticks_.argtypes = [ctypes.c_uint64]
+    L.rc_svc_set_idle_ticks_.restype = ctypes.c_int
+    assert L.rc_svc_set_idle_ticks_(ticks) == 0
+
+
+def test_service_wave_leaving_as_requests_arrive():
+    """a wave that leaves between the host's publication of a request and its
+    check must not read as a device fault.  With an idle time of 1 tick (10 ns) every wave
+    leaves right after its request, so nearly every call races a leaving wave; all of them must
+    return the reference's bytes and symbols (and no RC_E_DEVICE)."""
+    c2 = rc.Context(0)
+    _set_idle_ticks(1)
+    try:
+        syms, code, rets, out = _adaptive_round_trip(c2, n=400, seed=3)
+        assert code == R.encode_adaptive_stream(256, 32, 4000, 64, syms)
+        assert out == syms
+    finally:
+        _set_idle_ticks(0)
+        c2.close()
+
+
+def test_batch_launches_while_the_service_is_busy(ctx):
+    """while another thread keeps the context's service wave busy (it then lives up
+    to SVC_LIFE_MS = 2 s), batch encode / decode launches on torch's default stream and on a
+    second torch stream finish in their usual time: they do not queue behind the wave."""
+    import threading
+    import time
+    c2 = rc.Context(0)
+    c, cum, total = synth.zipf_table()
+    n, L = 2048, 4096
+    inv = synth.inverse_cdf(c)
+    syms = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    synth.fill(ctx, 0x5EED0001, inv, syms, L, n)
+    cap = rc.slot_capacity(L, 8.0)
+    so = torch.arange(n + 1, dtype=torch.int64, device="cuda") * L
+    oo = torch.arange(n + 1, dtype=torch.int64, device="cuda") * cap
+    out = torch.empty(n * cap, dtype=torch.uint8, device="cuda")
+    dec = torch.empty_like(syms)
+    ref = _adaptive_round_trip(c2, n=200, seed=5)
+
+    def batch(m):
+        t0 = time.perf_counter()
+        ol, fe = rc.encode_batch(m, syms, so, out, oo)
+        fd = rc.decode_batch(m, out, oo[:-1].contiguous(), ol, dec, so)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert int(fe.abs().sum()) == 0 and int(fd.abs().sum()) == 0 and torch.equal(dec, syms)
+        return dt
+
+    m_default = rc.StaticModel(c, cum, total, ctx=ctx)
+    m_c2 = rc.StaticModel(c, cum, total, ctx=c2)
+    base = max(batch(m_default), batch(m_c2))  # unloaded (and warmed up)
+    stop, errs, rounds = threading.Event(), [], [0]
+
+    def busy():
+        try:
+            while not stop.is_set():
+                if _adaptive_round_trip(c2, n=200, seed=5) != ref:
+                    errs.append("mismatch")
+                rounds[0] += 1
+        except Exception as e:  # (reported below)
+            errs.append(repr(e))
+
+    th = threading.Thread(target=busy)
+    th.start()
+    try:
+        time.sleep(0.3)
+        times = []
+        for m in (m_default, m_c2):
+            times.append(batch(m))
+            side = torch.cuda.Stream()
+            with torch.cuda.stream(side):
+                times.append(batch(m))
+    finally:
+        stop.set()
+        th.join()
+        c2.close()
+    assert not errs, errs
+    assert rounds[0] >= 1
+    # a launch queued behind the wave would wait for it to leave (>= its 5 ms idle after the
+    # busy thread's last call, up to 2 s): allow generous noise over the unloaded time
+    assert max(times) < max(0.5, 5 * base), (times, base)

@@ -38,7 +38,7 @@ def main():
     if a.config == "uniform":
         c, cum, total = synth.uniform_table()
     elif a.config == "adaptive128":
-        c, cum, total = synth.zipf_table(n=128, total=1 << 15)
+        c, cum, total = synth.zipf_table(n=128, total=1 << 16)
     else:
         c, cum, total = synth.zipf_table()
     if a.config.startswith("adaptive"):
