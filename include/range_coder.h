@@ -240,9 +240,11 @@ rc_status rc_stream_decode(rc_ctx* ctx, const uint32_t* c_dev, const uint32_t* c
  * *flags_out, and sticky ones in the state).
  * Small calls (request and result within 64 KiB) go to the context's stream-service wave: one
  * workgroup of one wave, launched by the first such call on a stream of its own, holding 64.4 KiB
- * of one CU's LDS, which polls a mailbox in pinned host memory and leaves 5 ms after its last
- * request (2 s after its launch at most; the next call launches another).  While it runs it
- * occupies that CU slot and its hardware queue like any resident kernel.  A call waits for the
+ * of one CU's LDS, which polls a mailbox in pinned host memory and leaves 0.25 ms after its last
+ * request, 1 ms after its launch at most, or as soon as a batch entry point of the library
+ * launches a kernel (the next call launches another wave).  While it runs it occupies that CU
+ * slot and its hardware queue like any resident kernel: a kernel of another library on a
+ * stream that shares that queue can wait up to 1 ms behind it.  A call waits for the
  * wave WITHOUT a time limit while the wave has not started (a wave waiting for a CU behind
  * long-running kernels is waited for, exactly as a launch would be); once the wave runs, a
  * call that sees no answer within 10 s returns RC_E_DEVICE and the context's service is off

@@ -271,4 +271,7 @@ struct RcKnobs {
   bool hist_hot;           // RC_HIST_HOT=0: the histogram without its ballot-counted hot symbol
 };
 RcKnobs rc_knobs_from_env();                      // rc_kernels.hip (rc_ctx_create only)
+// rc_resume.hip: ask the process's stream-service waves to leave before a batch launch (a
+// resident wave would hold the hardware queue its stream shares with the launch's)
+void rc_svc_yield_all_();
 const RcKnobs& rc_ctx_knobs_(const rc_ctx* ctx);  // rc_kernels.hip

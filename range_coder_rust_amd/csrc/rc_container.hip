@@ -308,6 +308,7 @@ rc_status rc_container_pack(rc_ctx* ctx, const rc_model* m, const uint8_t* slots
       mdev != dev)
     return RC_E_ARG;
   DevSet g(dev);
+  rc_svc_yield_all_();
   const u64 index_off = RC_CONTAINER_HEADER_BYTES + (kind == 0 ? hpad16(4ull * nsym) : 0);
   const u64 payload_off = index_off + 16ull * n_chunks;
   // scans: dst offsets of the padded streams, and the symbol total

@@ -521,6 +521,7 @@ rc_status rc_encode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* syms,
   if (m->device != ctx->device) return RC_E_ARG;
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
+  rc_svc_yield_all_();
   if (m->kind == 1) {
     const hipError_t e = rc_adaptive_encode_launch(ctx->cur, m->ap, syms, sym_off, n_chunks,
                                                    out, out_off, out_len, flags);
@@ -542,6 +543,7 @@ rc_status rc_decode_batch(rc_ctx* ctx, const rc_model* m, const uint8_t* code,
   if (m->device != ctx->device) return RC_E_ARG;
   DeviceGuard g(ctx->device);
   if (!g.ok) return RC_E_DEVICE;
+  rc_svc_yield_all_();
   if (m->kind == 1) {
     const hipError_t e = rc_adaptive_decode_launch(ctx->cur, m->ap, code, code_off, code_len,
                                                    syms_out, sym_off, n_chunks, flags);

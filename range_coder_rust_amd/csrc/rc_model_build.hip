@@ -218,6 +218,7 @@ rc_status rc_histogram(rc_ctx* ctx, const uint8_t* syms, const uint64_t* sym_off
   if (n_chunks == 0 || (!chunk_hist && !hist)) return RC_OK;
   if (!syms || !sym_off) return RC_E_ARG;
   DevSet g(dev);
+  rc_svc_yield_all_();
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return RC_E_DEVICE;

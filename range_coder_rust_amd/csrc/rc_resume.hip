@@ -300,18 +300,24 @@ __global__ __launch_bounds__(RWG) void k_stream_decode(
 // lanes, runs the same per-stream body as the launch path on lane 0 against the block in LDS
 // (so the body's loads and stores cost LDS latency, not device-memory round trips), writes the
 // result ranges back into the mailbox and sets `ack` (release).  It leaves on `stop`, after
-// SVC_IDLE_MS without a request, or after SVC_LIFE_MS in all, so it never outlives its caller
+// SVC_IDLE_US without a request, after SVC_LIFE_US in all, or when a launch of the library asks
+// it to yield (`yield_ep` = its epoch: rc_svc_yield_all_), so it never outlives its caller
 // for long: a later call starts a new one (an epoch: `alive` is 2 epoch + 1 while epoch's wave
 // runs and 2 epoch + 2 once it left).  Every exit condition is checked on every poll.
 // ------------------------------------------------------------------------------------------
-#define SVC_IDLE_MS 5
-#define SVC_LIFE_MS 2000
+// (short on purpose: a resident wave holds its hardware queue, and HIP maps the process's
+// streams onto 4 queues, so a kernel on another stream may sit behind the wave until it leaves;
+// the library's own launches ask it to leave first, rc_svc_yield_all_)
+#define SVC_IDLE_US 250
+#define SVC_LIFE_US 1000
 #define SVC_BLOCK (64u << 10)  // request / result block bytes (larger calls take the launch path)
 #define SVC_STOP 0xFFFFFFFFu   // a seq value: leave now (a request number never reaches it)
 enum { SVC_ENCODE = 1, SVC_DECODE = 2 };
 
 struct alignas(64) SvcBox {
-  u32 seq, p0[15];    // host -> wave: request number (written last)
+  u32 seq;            // host -> wave: request number (written last)
+  u32 yield_ep;       // host -> wave: the wave of this epoch leaves (read with seq, one load)
+  u32 p0[14];
   u32 ack, p1[15];    // wave -> host: the last request done
   u32 alive, p2[15];  // wave: 2 epoch + 1 running, 2 epoch + 2 left
   u32 stop, p3[15];   // host: leave now
@@ -328,6 +334,9 @@ static_assert(sizeof(SvcBox) == 384, "mailbox header layout");
 static_assert(sizeof(SvcBox) + SVC_BLOCK <= 96u << 10, "service LDS block");
 
 static __device__ __forceinline__ u32 sys_load(const u32* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+static __device__ __forceinline__ u64 sys_load64(const u64* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 static __device__ __forceinline__ void sys_store(u32* p, u32 v) {
@@ -376,9 +385,11 @@ __global__ __launch_bounds__(RWG) void k_stream_service(SvcBox* box, u32 epoch, 
   for (;;) {
     // one load per poll: `stop` is rc_ctx_destroy's (checked every 64 polls), seq == SVC_STOP
     // is the same request from a caller that holds the mailbox
-    const u32 seq = __builtin_amdgcn_readfirstlane(sys_load(&box->seq));
+    const u64 sy = sys_load64((const u64*)&box->seq);  // {seq, yield_ep}
+    const u32 seq = __builtin_amdgcn_readfirstlane((u32)sy);
+    const u32 ye = __builtin_amdgcn_readfirstlane((u32)(sy >> 32));
     const u64 now = __builtin_amdgcn_s_memrealtime();
-    if (seq == SVC_STOP || now - t0 > life_ticks) break;
+    if (seq == SVC_STOP || ye == epoch || now - t0 > life_ticks) break;
     if ((++polls & 63) == 0 && __builtin_amdgcn_readfirstlane(sys_load(&box->stop))) break;
     if (seq == done) {
       if (now - tl > idle_ticks) break;
@@ -529,9 +540,9 @@ struct Svc {
 std::mutex g_svc_mu;
 std::unordered_map<const rc_ctx*, std::shared_ptr<Svc>> g_svcs;
 // at process exit, tell any running wave to leave (no HIP calls: the runtime may be going too;
-// a wave leaves within one poll, and by SVC_IDLE_MS in any case).  The box is written only under
+// a wave leaves within one poll, and by SVC_IDLE_US in any case).  The box is written only under
 // its service's lock, which a call that times out holds while it frees the box; a service whose
-// lock another thread holds is skipped (its wave leaves by itself after SVC_IDLE_MS).
+// lock another thread holds is skipped (its wave leaves by itself after SVC_IDLE_US).
 struct SvcAtExit {
   ~SvcAtExit() {
     std::lock_guard<std::mutex> g(g_svc_mu);
@@ -549,12 +560,13 @@ struct SvcAtExit {
 bool svc_enabled(const rc_ctx* ctx) { return rc_ctx_knobs_(ctx).stream_service; }
 
 // Test hook (tests/test_gpu_stream.py, not in include/range_coder.h): the wave's idle time in
-// 10-ns ticks for the waves launched from now on (0: SVC_IDLE_MS), so a test can make waves
+// 10-ns ticks for the waves launched from now on (0: SVC_IDLE_US), so a test can make waves
 // leave at the moment requests are published.
 std::atomic<u64> g_svc_idle_ticks{0};
+std::atomic<bool> g_svc_any{false};  // some service wave was ever launched (rc_svc_yield_all_)
 u64 idle_ticks() {
   const u64 t = g_svc_idle_ticks.load(std::memory_order_relaxed);
-  return t ? t : (u64)SVC_IDLE_MS * 100000ull;
+  return t ? t : (u64)SVC_IDLE_US * 100ull;
 }
 
 std::shared_ptr<Svc> svc_get(const rc_ctx* ctx) {
@@ -636,13 +648,14 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, int dev, Fill fill, rc_status* err) {
       ++sv->epoch;
       hipLaunchKernelGGL(k_stream_service, dim3(1), dim3(RWG), 0, sv->stream, sv->dbox_host,
                          sv->epoch, idle_ticks(),
-                         (u64)SVC_LIFE_MS * 100000ull);
+                         (u64)SVC_LIFE_US * 100ull);
       if (hipGetLastError() != hipSuccess) {
         sv->broken = true;
         *err = RC_E_DEVICE;
         return true;
       }
       sv->launched = true;
+      g_svc_any.store(true, std::memory_order_relaxed);
     }
     if ((spin & 1023) == 1023) {
       // The timeout runs only while the current epoch's wave runs: a wave still waiting for a
@@ -670,6 +683,23 @@ bool svc_call(const rc_ctx* ctx, Svc* sv, int dev, Fill fill, rc_status* err) {
 
 }  // namespace
 
+// Every launch of a batch kernel by the library first asks the process's running service waves
+// to leave (their yield_ep := their epoch): such a wave may hold the hardware queue that the
+// batch kernel's stream maps to, and the batch kernel would otherwise wait up to SVC_LIFE_US
+// behind it.  The next per-call request launches a new wave.  A service whose lock a call
+// holds is skipped (its wave is serving that call, and leaves by SVC_LIFE_US at the latest).
+void rc_svc_yield_all_() {
+  if (!g_svc_any.load(std::memory_order_relaxed)) return;
+  std::lock_guard<std::mutex> g(g_svc_mu);
+  for (auto& kv : g_svcs) {
+    Svc* sv = kv.second.get();
+    if (!sv) continue;
+    std::unique_lock<std::mutex> lk(sv->mu, std::try_to_lock);
+    if (lk.owns_lock() && sv->box && sv->launched)
+      __atomic_store_n(&sv->box->yield_ep, sv->epoch, __ATOMIC_RELEASE);
+  }
+}
+
 extern "C" {
 
 rc_status rc_ctx_stream_(rc_ctx* ctx, hipStream_t* s, int* device);  // rc_kernels.hip
@@ -684,6 +714,7 @@ rc_status rc_stream_encode(rc_ctx* ctx, rc_stream_state* states, const uint32_t*
   if (n_streams == 0) return RC_OK;
   if (!states || !triples || !sym_off || !out || !out_off || !out_len || !flags) return RC_E_ARG;
   Dev g(dev);
+  rc_svc_yield_all_();
   hipLaunchKernelGGL(k_stream_encode, dim3((n_streams + RWG - 1) / RWG), dim3(RWG), 0, s,
                      states, triples, sym_off, n_streams, out, out_off, out_len, nbytes, finish,
                      flags);
@@ -703,6 +734,7 @@ rc_status rc_stream_decode(rc_ctx* ctx, const uint32_t* c, const uint32_t* cum,
   if (!c || !cum || !states || !code || !code_off || !code_len || !syms || !sym_off || !flags)
     return RC_E_ARG;
   Dev g(dev);
+  rc_svc_yield_all_();
   hipLaunchKernelGGL(k_stream_decode, dim3((n_streams + RWG - 1) / RWG), dim3(RWG), 0, s, c,
                      cum, n_symbols, total_freq, states, code, code_off, code_len, syms, sym_off,
                      n_streams, flags);
