@@ -43,15 +43,14 @@ def build(ops):
 
 def run(out, ops, rounds):
     os.makedirs(out, exist_ok=True)
-    args = ["--no-cpu-baseline", "--no-zipf", "--no-adaptive", "--no-model-build",
-            "--no-container", "--no-host-stream", "--steps", "3", "--warmup", "1"]
+    args = ["--config", os.environ.get("FILL_CONFIG", "uniform"), "--steps", "3", "--warmup", "1"]
     res = {}
     for r in range(rounds):
         for op in ["base"] + list(ops):
             env = dict(os.environ)
             if op != "base":
                 env["RC_LIB_PATH"] = lib(op)
-            p = subprocess.run([sys.executable, "bench.py"] + args, cwd=ROOT, env=env,
+            p = subprocess.run([sys.executable, "tools/kbench.py"] + args, cwd=ROOT, env=env,
                                capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
                 sys.stderr.write(p.stderr[-2000:])

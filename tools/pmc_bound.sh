@@ -12,13 +12,11 @@ O="$ROOT/gpurun_out/bound_$TAG"
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 cd "$ROOT"
-ONE=(--no-cpu-baseline --no-zipf --no-adaptive --no-model-build --no-container --no-host-stream
-     --steps 1 --warmup 0)
 for cfg in ${CONFIGS:-uniform zipf}; do
   if [ "$cfg" = shard ]; then
-    RUN=(python3 bench.py --config zipf --global-chunks 131072 "${ONE[@]}")
+    RUN=(python3 tools/kbench.py --config zipf --chunks 131072 --steps 1 --warmup 0)
   else
-    RUN=(python3 bench.py --config $cfg "${ONE[@]}")
+    RUN=(python3 tools/kbench.py --config $cfg --steps 1 --warmup 0)
   fi
   mkdir -p "$O/$cfg"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/$cfg/trace" -o run --output-format csv \

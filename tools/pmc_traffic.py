@@ -91,7 +91,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("run", help="gpurun_out/prof_<tag> directory")
     p.add_argument("--tag", required=True)
-    p.add_argument("--config", default="uniform")
+    p.add_argument("--config", default="zipf")
     p.add_argument("--chunks", type=int, default=1 << 20)
     p.add_argument("--chunk-bytes", type=int, default=65536)
     a = p.parse_args()
@@ -125,7 +125,11 @@ def main():
     with open(os.path.join(a.run, "lib.sha256")) as f:
         lib_sha = f.read().split()[0]
     n_sym = a.chunks * a.chunk_bytes
-    alg = bench["roofline"]["alg_bytes_per_launch"]
+    # algorithmic bytes of the counted workload (profile.sh's plain kbench.py run of it)
+    with open(os.path.join(a.run, "kbench.json")) as f:
+        kb = json.loads([l for l in f if l.startswith("{")][-1])
+    assert kb["config"] == a.config and kb["chunks"] == a.chunks, (kb, a.config, a.chunks)
+    alg = kb["alg_bytes"]
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     for dom, cs in pmc.items():

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Profile the default bench on the GPU box; everything lands under gpurun_out/prof_<tag>/.
 #   gpurun -- 'bash tools/profile.sh r02'
-# then, locally: python tools/pmc_traffic.py gpurun_out/prof_r02 --tag r02
+# then, locally: python tools/pmc_traffic.py gpurun_out/prof_r02 --tag r02 --config zipf
 # (writes profiles/traffic.json and profiles/r02/*, which bench.py and DESIGN.md cite).
 # Each pass is its own rocprofv3 run: kernel trace + stats of the exact default bench command,
 # then counter passes (counters are never combined with trace domains; at most 4 TCC counters
@@ -18,9 +18,9 @@ mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 cd "$ROOT"
 sha256sum range_coder_rust_amd/librc_amd.so > "$O/lib.sha256"  # (pmc_traffic.py keys traffic.json to it)
-# the PMC passes replay the headline workload once (no Zipf leg, no CPU sample): one launch each
-PMC=(python3 bench.py --no-cpu-baseline --no-zipf --no-adaptive --no-model-build --no-container
-     --no-host-stream --steps 1 --warmup 0)
+# the PMC passes replay one configuration's encode and decode once (CONFIG: zipf, the headline,
+# or uniform): one launch of each kernel
+PMC=(python3 tools/kbench.py --config "${CONFIG:-zipf}" --steps 1 --warmup 0)
 CAL=("$ROOT/tools/pmc_calib")
 PASSES=("FETCH_SIZE" "WRITE_SIZE"
         "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum"
@@ -29,6 +29,8 @@ PASSES=("FETCH_SIZE" "WRITE_SIZE"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv \
   -- python3 bench.py > "$O/bench.json" 2> "$O/bench.err"
 echo "trace pass done"
+# the counter passes' workload once without a profiler: its algorithmic bytes per launch
+timeout -k 10 300 "${PMC[@]}" > "$O/kbench.json" 2> "$O/kbench.err"
 i=0
 for p in "${PASSES[@]}"; do
   # shellcheck disable=SC2086
