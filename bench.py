@@ -411,21 +411,26 @@ def kernel_stats(n_sym, code_bytes, ms):
 
 
 def traffic_for(path, key):
-    """(HBM bytes per launch, note) from tools/pmc_traffic.py's file, only when the entry was
-    profiled on this exact librc_amd.so (keyed by its sha256)."""
+    """(counted bytes per launch, note, HBM-side estimate) from tools/pmc_traffic.py's file, only
+    when the entry was profiled on this exact librc_amd.so (keyed by its sha256).  Counted =
+    the TCC->EA request bytes (Infinity-Cache hits included: no counter separates them on this
+    stack); the estimate takes the read side at its first touches."""
     note = "no profile of this workload in " + os.path.relpath(path, ROOT)
     try:
         with open(path) as f:
             tr = json.load(f)
     except (OSError, ValueError):
-        return None, note
+        return None, note, None
     if key not in tr:
-        return None, note
+        return None, note, None
     from range_coder_rust_amd import _native
     e = tr[key]
     if e.get("lib_sha256") != lib_sha256(_native.LIB_PATH):
-        return None, f"stale: {e.get('round')} profiled another build of librc_amd.so; not reported"
-    return e["hbm_bytes_per_launch"], f"PMC, this build ({e.get('round')})"
+        return (None, f"stale: {e.get('round')} profiled another build of librc_amd.so; "
+                      f"not reported", None)
+    return (e["hbm_bytes_per_launch"],
+            f"PMC TCC->EA request bytes, this build ({e.get('round')})",
+            e.get("hbm_estimate_per_launch"))
 
 
 def main():
@@ -465,11 +470,12 @@ def main():
             "decode": kernel_stats(n * L, res["code_bytes"], res["dec_ms"])}
     dom = "decode" if res["dec_ms"] >= res["enc_ms"] else "encode"
     # roofline.traffic: PMC-measured HBM bytes of this exact library build only
-    traffic, traffic_note = traffic_for(args.traffic, f"zipf:{n}:{L}:{dom}")
+    traffic, traffic_note, traffic_est = traffic_for(args.traffic, f"zipf:{n}:{L}:{dom}")
     achieved = kern[dom]["gbps"]
     roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBPS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic,
-                    traffic_source=traffic_note, kernel=f"{dom} (Zipf(1.2), LUT 4)",
+                    traffic_source=traffic_note, traffic_hbm_estimate=traffic_est,
+                    kernel=f"{dom} (Zipf(1.2), LUT 4)",
                     alg_bytes_per_launch=kern[dom]["alg_bytes"])
     # N > 1: achieved / peak above is one rank's kernel against one GPU; the aggregate is every
     # rank's algorithmic bytes over the slowest rank's kernel time against N GPUs' peak
@@ -489,7 +495,7 @@ def main():
         ur = run_leg(torch, dist, u, us, 1, world)
         ue = kernel_stats(wn * L, ur["code_bytes"], ur["enc_ms"])
         ud = kernel_stats(wn * L, ur["code_bytes"], ur["dec_ms"])
-        utr, utr_note = traffic_for(args.traffic, f"uniform:{wn}:{L}:decode")
+        utr, utr_note, utr_est = traffic_for(args.traffic, f"uniform:{wn}:{L}:decode")
         extras["uniform_weak"] = dict(
             workload=f"configs[1] on every rank: {wn} x {L // 1024} KiB chunks per GPU, "
                      f"uniform-256 static model (c = 1, total 256; weak scaling)",
@@ -499,6 +505,7 @@ def main():
             bytes_per_symbol=round(ur["code_bytes"] / (wn * L), 5),
             roofline_frac_encode=round(ue["frac"], 4), roofline_frac_decode=round(ud["frac"], 4),
             decode_traffic=utr, decode_traffic_source=utr_note,
+            decode_traffic_hbm_estimate=utr_est,
             bit_exact_round_trip=ur["ok"])
     if world == 1:
         if not args.no_model_build:

@@ -53,6 +53,9 @@
 #ifndef ENC_PAIR
 #define ENC_PAIR 1           // small-model encoders test the rare path once per two symbols
 #endif
+#ifndef DEC_SEL_FILL
+#define DEC_SEL_FILL 1       // LUT 4 (pow2): the select's wait states do useful work (round 6)
+#endif
 #ifndef DEC_CHECK_SPAN
 #define DEC_CHECK_SPAN 8     // small-model decoders: symbols between ring checks in a phase
 #endif

@@ -26,9 +26,11 @@ PASSES=("FETCH_SIZE" "WRITE_SIZE"
         "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum"
         "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum TCC_EA0_RDREQ_DRAM_32B_sum")
 
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv \
-  -- python3 bench.py > "$O/bench.json" 2> "$O/bench.err"
-echo "trace pass done"
+if [ -z "${SKIP_TRACE:-}" ]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv \
+    -- python3 bench.py > "$O/bench.json" 2> "$O/bench.err"
+  echo "trace pass done"
+fi
 # the counter passes' workload once without a profiler: its algorithmic bytes per launch
 timeout -k 10 300 "${PMC[@]}" > "$O/kbench.json" 2> "$O/kbench.err"
 i=0
