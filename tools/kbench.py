@@ -27,6 +27,8 @@ def main():
     p.add_argument("--chunk-bytes", type=int, default=65536)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--zipf-s", type=float, default=1.2, help="zipf: the exponent")
+    p.add_argument("--zipf-total", type=int, default=1 << 16, help="zipf: the table's total")
     p.add_argument("--first-chunk", type=int, default=0,
                    help="global index of this run's first chunk (a shard of the bench stream)")
     a = p.parse_args()
@@ -40,7 +42,7 @@ def main():
     elif a.config == "adaptive128":
         c, cum, total = synth.zipf_table(n=128, total=1 << 16)
     else:
-        c, cum, total = synth.zipf_table()
+        c, cum, total = synth.zipf_table(s=a.zipf_s, total=a.zipf_total)
     if a.config.startswith("adaptive"):
         m = rc.AdaptiveModel(len(c), **rc.ADAPTIVE_DEFAULTS, ctx=ctx)
         bits = 6.0 if a.config == "adaptive" else 5.5
@@ -77,7 +79,7 @@ def main():
     for i in range(0, n * L, 1 << 30):
         ok = ok and torch.equal(dec[i:i + (1 << 30)], syms[i:i + (1 << 30)])
     code = int(ol.sum())
-    res = dict(config=a.config, chunks=n, chunk_bytes=L, steps=a.steps,
+    res = dict(config=a.config, chunks=n, table_total=int(total), chunk_bytes=L, steps=a.steps,
                encode_ms=round(enc, 3), decode_ms=round(dcd, 3),
                encode_gsym_s=round(n * L / enc / 1e6, 3) if enc else None,
                decode_gsym_s=round(n * L / dcd / 1e6, 3) if dcd else None,
