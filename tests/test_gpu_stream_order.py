@@ -109,3 +109,63 @@ def test_reset_stream_then_synchronize_through_the_c_abi():
     fd2 = rc.decode_batch(m, out, co, ol, dec, so)
     torch.cuda.synchronize()
     assert not fd2.any()
+
+
+def test_batch_round_trips_from_concurrent_host_threads():
+    """One context per host thread (include/range_coder.h), each on its own torch stream with
+    its own model (uniform, Zipf, a random table with a non-power-of-two total): concurrent
+    model creation, encode and decode; every thread's bytes against the oracle and its decode
+    against its input.  The reference's coders are independent Send state machines
+    (encoder.rs:7-20, decoder.rs:6-23): parallelism is independent instances."""
+    import threading
+
+    n_threads, n_ch, ln, reps = 4, 64, 16384, 3
+    rng = np.random.default_rng(11)
+    tables = [synth.uniform_table(), synth.zipf_table()]
+    while len(tables) < n_threads:
+        c = rng.integers(1, 400, 256).astype(np.uint32)
+        tables.append((c, np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.uint32),
+                       int(c.sum())))
+    results, errors = [None] * n_threads, []
+    start = threading.Barrier(n_threads)
+
+    def work(t):
+        try:
+            c, cum, total = tables[t]
+            ctx = rc.Context(0)
+            s = torch.cuda.Stream()
+            start.wait()
+            with torch.cuda.stream(s):
+                m = rc.StaticModel(c, cum, total, ctx=ctx)
+                cap = rc.slot_capacity(ln, 12.0)
+                syms = torch.empty(n_ch * ln, dtype=torch.uint8, device="cuda")
+                synth.fill(ctx, 0x5EED0900 + t, synth.inverse_cdf(c), syms, ln, n_ch)
+                so = torch.arange(n_ch + 1, dtype=torch.int64, device="cuda") * ln
+                oo = torch.arange(n_ch + 1, dtype=torch.int64, device="cuda") * cap
+                out = torch.empty(n_ch * cap, dtype=torch.uint8, device="cuda")
+                dec = torch.empty_like(syms)
+                ok = True
+                for _ in range(reps):
+                    ol, fe = rc.encode_batch(m, syms, so, out, oo)
+                    fd = rc.decode_batch(m, out, oo[:-1].contiguous(), ol, dec, so)
+                    ok = ok and bool(torch.equal(dec, syms)) and not fe.any() and not fd.any()
+                s.synchronize()
+                results[t] = (ok, syms.cpu().numpy(), out.cpu().numpy(), ol.cpu().numpy(), cap)
+            m.close()
+            ctx.close()
+        except Exception as exc:  # noqa: BLE001 (reported below)
+            errors.append((t, repr(exc)))
+
+    threads = [threading.Thread(target=work, args=(t,)) for t in range(n_threads)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not errors, errors
+    from oracle import cpu
+    for t, (ok, h, hb, hl, cap) in enumerate(results):
+        assert ok, f"thread {t}: round trip"
+        c, cum, total = tables[t]
+        for k in (0, n_ch - 1):
+            f, b, _ = cpu.encode(c, cum, total, h[k * ln:(k + 1) * ln])
+            assert f == 0 and bytes(hb[k * cap:k * cap + int(hl[k])]) == b, f"thread {t} chunk {k}"
