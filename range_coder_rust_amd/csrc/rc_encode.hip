@@ -95,17 +95,28 @@ struct EncOut {
   u32 lo_ok, hi_ok;  // writable byte window [lo_ok, hi_ok) relative to gbase
 };
 
-// One flush round.  Lane L of the wave moves granule (L & 3) of the unit of chunk 16*i + L/4
-// for i = 0..3; chunks with has == false are masked.  Granules touching the slot edges are
-// written byte by byte (first unit of a misaligned slot, capacity end).
+// One flush round.  The chunks of the wave that hold a complete 64-B unit (`has`) are ranked
+// (v_mbcnt over their ballot) and their lane numbers listed in the wave's LDS rank table, so
+// the round runs ceil(ready / 16) steps instead of 4: in step j, lane L moves granule (L & 3) of
+// the unit of the (16 j + L/4)-th ready chunk.  Granules touching the slot edges are written
+// byte by byte (first unit of a misaligned slot, capacity end).
 static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, const u32* wring,
-                                                 const EncOut* wout) {
+                                                 const EncOut* wout, u32* wrank) {
+  const u64 M = __builtin_amdgcn_ballot_w64(has);
+  const u32 ready = (u32)__builtin_popcountll(M);  // (wave-uniform: s_bcnt1)
+  if (has) {
+    const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(M >> 32), __builtin_amdgcn_mbcnt_lo((u32)M, 0u));
+    wrank[r] = lane;
+  }
+  const u32 g = lane & 3;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const u32 c = 16 * i + (lane >> 2), g = lane & 3;
-    const bool hc = __shfl((int)has, c) != 0;
+  for (u32 j = 0; j < 4; ++j) {
+    if (16 * j >= ready) break;  // (wave-uniform)
+    const u32 k = 16 * j + (lane >> 2);
+    const bool act = k < ready;
+    const u32 c = act ? wrank[k] : 0u;
     const u32 fp = (u32)__shfl((int)e.fpos, c);
-    if (hc) {
+    if (act) {
       // fp is a multiple of ENC_UNIT = 64 B, so the granule's first slot is a multiple of 4 and
       // its 4 dwords never wrap the ring: one address, two ds_read2 (st64 for column-major)
       const u32 slot = ((fp >> 2) + 4 * g) & (ENC_RING - 1);
@@ -125,9 +136,9 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
       } else {
         const u32 w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const u32 p = p0 + j;
-          if (p >= o.lo_ok && p < o.hi_ok) gstore8(o.gbase + p, w[j >> 2] >> (8 * (j & 3)));
+        for (int b = 0; b < 16; ++b) {
+          const u32 p = p0 + b;
+          if (p >= o.lo_ok && p < o.hi_ok) gstore8(o.gbase + p, w[b >> 2] >> (8 * (b & 3)));
         }
       }
     }
@@ -137,12 +148,12 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
 
 // flush rounds until no lane's ring is above the threshold (wave-uniform call sites only)
 static __device__ __forceinline__ void enc_flush(Enc& e, u32 lane, const u32* wring,
-                                                 const EncOut* wout) {
+                                                 const EncOut* wout, u32* wrank) {
   // (the first test stays inline in every caller: written as a plain while loop, the compiler
   // shared one test block among the call sites and copied the coder state at each jump to it)
   if (__builtin_expect(__any((int)enc_ready(e, FLUSH_AT)), 0)) {
     do {
-      enc_round(e, enc_ready(e, ENC_UNIT), lane, wring, wout);
+      enc_round(e, enc_ready(e, ENC_UNIT), lane, wring, wout, wrank);
     } while (__any((int)enc_ready(e, FLUSH_AT)));
   }
 }
@@ -268,12 +279,13 @@ static __device__ __forceinline__ bool enc_step(Enc& e, const ModelArgs& m, uint
 // flush
 template <int DIV, int SM>
 static __device__ __forceinline__ void enc_sym(Enc& e, const ModelArgs& m, uint2 t, bool act,
-                                               u32 lane, const u32* wring, const EncOut* wout) {
+                                               u32 lane, const u32* wring, const EncOut* wout,
+                                               u32* wrank) {
   bool rare = false;
   if (act) rare = enc_step<DIV, SM>(e, m, t);
   if (__builtin_expect(__any((int)rare), 0)) {
     if (rare) enc_rare(e);
-    enc_flush(e, lane, wring, wout);
+    enc_flush(e, lane, wring, wout, wrank);
   }
 }
 
@@ -286,7 +298,7 @@ static __device__ __forceinline__ void enc_sym(Enc& e, const ModelArgs& m, uint2
 template <int DIV, int SM>
 static __device__ __forceinline__ void enc_sym2(Enc& e, const ModelArgs& m, uint2 t0, uint2 t1,
                                                 bool act, u32 lane, const u32* wring,
-                                                const EncOut* wout) {
+                                                const EncOut* wout, u32* wrank) {
   bool r0 = false, r1 = false;
   if (act) r0 = enc_step<DIV, SM>(e, m, t0);
   const Enc ea = e;
@@ -298,7 +310,7 @@ static __device__ __forceinline__ void enc_sym2(Enc& e, const ModelArgs& m, uint
       r1 = enc_step<DIV, SM>(e, m, t1);
     }
     if (r1) enc_rare(e);
-    enc_flush(e, lane, wring, wout);
+    enc_flush(e, lane, wring, wout, wrank);
   }
 }
 
@@ -308,7 +320,7 @@ static __device__ __forceinline__ void enc_sym2(Enc& e, const ModelArgs& m, uint
 template <int DIV, int SM>
 static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const uint2* s_tab,
                                              uint4 v, bool act, u32 lane, const u32* wring,
-                                             const EncOut* wout) {
+                                             const EncOut* wout, u32* wrank) {
   // the words rotate down (w0 holds the current 4 symbols) instead of being indexed: a rolled
   // loop would select w[i >> 2] with v_cndmask_b32 on VCC (~13 extra SIMD cycles each)
   u32 w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
@@ -322,7 +334,7 @@ static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const u
         const uint2 t1 = s_tab[(w0 >> (8 * (i + 1))) & 255u];
         const u32 sn = i < 2 ? (w0 >> (8 * (i + 2))) & 255u : w1 & 255u;
         const uint2 tn = s_tab[sn];  // (past the tile's end: a harmless extra read)
-        enc_sym2<DIV, SM>(e, m, t, t1, act, lane, wring, wout);
+        enc_sym2<DIV, SM>(e, m, t, t1, act, lane, wring, wout, wrank);
         t = tn;
       }
     } else {
@@ -330,11 +342,11 @@ static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const u
       for (int i = 0; i < 4; ++i) {
         const u32 sn = i < 3 ? (w0 >> (8 * (i + 1))) & 255u : w1 & 255u;
         const uint2 tn = s_tab[sn];  // (past the tile's end: a harmless extra read)
-        enc_sym<DIV, SM>(e, m, t, act, lane, wring, wout);
+        enc_sym<DIV, SM>(e, m, t, act, lane, wring, wout, wrank);
         t = tn;
       }
     }
-    if (q & 1) enc_flush(e, lane, wring, wout);
+    if (q & 1) enc_flush(e, lane, wring, wout, wrank);
     w0 = w1;
     w1 = w2;
     w2 = w3;
@@ -346,9 +358,9 @@ template <int DIV, int SM>
 static __device__ __forceinline__ void enc_byte_sym(Enc& e, const ModelArgs& m,
                                                     const uint2* s_tab, const uint8_t* sp, u64 i,
                                                     bool act, u32 lane, const u32* wring,
-                                                    const EncOut* wout) {
+                                                    const EncOut* wout, u32* wrank) {
   const u32 sym = act ? (u32)sp[i] : 0u;
-  enc_sym<DIV, SM>(e, m, s_tab[sym], act, lane, wring, wout);
+  enc_sym<DIV, SM>(e, m, s_tab[sym], act, lane, wring, wout, wrank);
 }
 
 // the first symbol of a chunk the reference cannot encode (rare: flagged chunks only)
@@ -374,6 +386,7 @@ __global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, co
   // (1-KiB aligned: a column base has no bits in the row field, ENC_ROWS)
   __shared__ __attribute__((aligned(1024))) u32 s_ring[WAVES * ENC_RING * 64];
   __shared__ EncOut s_out[WG];
+  __shared__ u32 s_rank[WG];  // per wave: the lanes holding a unit, by rank (flush rounds)
   const u32 tid = threadIdx.x;
   {
     // SM (cum < 2^16): a symbol the reference cannot encode (c == 0: endless loop; outside the
@@ -413,6 +426,7 @@ __global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, co
   __syncthreads();
   const u32* wring = s_ring + wave * ENC_RING * 64;
   const EncOut* wout = s_out + wave * 64;
+  u32* const wrank = s_rank + wave * 64;
 
   Enc e;
 #ifdef RC_FILL
@@ -433,8 +447,8 @@ __global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, co
   const u64 ntile = (n - head) >> 6;
   // head: byte-wise, all lanes in step (flush rounds are wave-wide)
   for (u64 i = 0; __any((int)(i < head)); ++i) {
-    enc_byte_sym<DIV, SM>(e, m, s_tab, sp, i, i < head, lane, wring, wout);
-    if ((i & 7) == 7) enc_flush(e, lane, wring, wout);
+    enc_byte_sym<DIV, SM>(e, m, s_tab, sp, i, i < head, lane, wring, wout, wrank);
+    if ((i & 7) == 7) enc_flush(e, lane, wring, wout, wrank);
   }
   // body, part 1: the tiles every live lane of the wave has, with every lane active (no
   // per-symbol exec masking).  Dead lanes run along on a dummy tile (g_sink, zeros) and a slot
@@ -476,11 +490,11 @@ __global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, co
         n3 = q[3];
       }
     }
-    enc16<DIV, SM>(e, m, s_tab, c0, true, lane, wring, wout);
-    enc16<DIV, SM>(e, m, s_tab, c1, true, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, c0, true, lane, wring, wout, wrank);
+    enc16<DIV, SM>(e, m, s_tab, c1, true, lane, wring, wout, wrank);
     if (ENC_TILE_Q == 4) {
-      enc16<DIV, SM>(e, m, s_tab, c2, true, lane, wring, wout);
-      enc16<DIV, SM>(e, m, s_tab, c3, true, lane, wring, wout);
+      enc16<DIV, SM>(e, m, s_tab, c2, true, lane, wring, wout, wrank);
+      enc16<DIV, SM>(e, m, s_tab, c3, true, lane, wring, wout, wrank);
     }
     c0 = n0;
     c1 = n1;
@@ -493,12 +507,13 @@ __global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, co
     const bool act = b < nblk;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (act) v = tp[b];
-    enc16<DIV, SM>(e, m, s_tab, v, act, lane, wring, wout);
+    enc16<DIV, SM>(e, m, s_tab, v, act, lane, wring, wout, wrank);
   }
   const u64 tail0 = head + (ntile << 6);
   for (u64 j = 0; __any((int)(tail0 + j < n)); ++j) {  // j is wave-uniform
-    enc_byte_sym<DIV, SM>(e, m, s_tab, sp, tail0 + j, tail0 + j < n, lane, wring, wout);
-    if ((j & 7) == 7) enc_flush(e, lane, wring, wout);
+    enc_byte_sym<DIV, SM>(e, m, s_tab, sp, tail0 + j, tail0 + j < n, lane, wring, wout,
+                          wrank);
+    if ((j & 7) == 7) enc_flush(e, lane, wring, wout, wrank);
   }
 
   // Encoder::finish (encoder.rs:40-46): 8 x left_shift
@@ -516,7 +531,7 @@ __global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, co
   // final rounds: the last (partial) units, clipped to the stream end
   const u32 end = a + len;
   if (end < s_out[tid].hi_ok) s_out[tid].hi_ok = end;
-  while (__any((int)(e.fpos < wend))) enc_round(e, e.fpos < wend, lane, wring, wout);
+  while (__any((int)(e.fpos < wend))) enc_round(e, e.fpos < wend, lane, wring, wout, wrank);
   RC_STAMP_END(enc, blockIdx.x * WAVES + wave, lane, n);
   if (live) {
     if (SM == 1) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;

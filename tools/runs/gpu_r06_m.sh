@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 6: the compacted-flush encoder variant against the in-tree library again, 4 rounds with
+# the order alternating (flushc first in even rounds)
+set -euo pipefail
+O=gpurun_out/r06m; mkdir -p $O
+for r in 1 2 3 4; do
+  if [ $((r % 2)) = 0 ]; then order="flushc default"; else order="default flushc"; fi
+  for lib in $order; do
+    L=""; [ $lib != default ] && L=$PWD/variants/librc_amd_$lib.so
+    for cfg in uniform zipf; do
+      RC_LIB_PATH=$L timeout -k 10 300 python3 tools/kbench.py --config $cfg --steps 5 --warmup 1 \
+        > $O/${lib}_${cfg}_$r.json 2> $O/${lib}_${cfg}_$r.err
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['encode_gsym_s'], d['decode_gsym_s'], 'exact' if d['bit_exact_round_trip'] else 'MISMATCH')" $O/${lib}_${cfg}_$r.json $lib.$cfg.$r
+    done
+  done
+done
