@@ -65,7 +65,8 @@ struct Enc {
   u64 acc;         // settled bytes, newest in the low bits; the B & 31 lowest are not pushed
   u32 B;           // bit position of the next settled byte, from the 64-B aligned slot base:
                    // dword B >> 5 of the stream is the incomplete one (its ring slot is free)
-  u32 fpos;        // byte position of the next unit to store
+  u32 fthr;        // 8 (fpos + FLUSH_AT), fpos the byte position of the next unit to store:
+                   // the flush test is one compare against B (enc_ready)
 #ifdef RC_FILL
   rc_fill_t fill;  // scratch builds: the filler instructions' register
 #endif
@@ -83,10 +84,14 @@ static __device__ __forceinline__ void ring_put(u32 col, u32 slot, u32 v) {
 // byte position of the incomplete dword (everything below it has been pushed to the ring)
 static __device__ __forceinline__ u32 enc_wpos(const Enc& e) { return (e.B >> 5) << 2; }
 
-// enc_wpos(e) - fpos >= T for T a multiple of 4, tested as (B >> 3) - fpos >= T: fpos + T is a
-// multiple of 4, so rounding B >> 3 down to one (enc_wpos) cannot cross it (one shift fewer)
+// byte position of the next unit to store
+static __device__ __forceinline__ u32 enc_fpos(const Enc& e) { return (e.fthr >> 3) - FLUSH_AT; }
+
+// enc_wpos(e) - fpos >= T for T a multiple of 4, tested as B >= 8 (fpos + T): fpos + T is a
+// multiple of 4, so rounding B >> 3 down to one (enc_wpos) cannot cross it; against the kept
+// threshold fthr = 8 (fpos + FLUSH_AT) that is one compare (T = FLUSH_AT) or an add and one
 static __device__ __forceinline__ bool enc_ready(const Enc& e, u32 T) {
-  return (e.B >> 3) - e.fpos >= T;
+  return e.B >= e.fthr - 8u * (FLUSH_AT - T);
 }
 
 // Per-chunk output geometry shared with the other lanes of the wave (flush rounds)
@@ -96,9 +101,9 @@ struct EncOut {
 };
 
 // One flush round.  The chunks of the wave that hold a complete 64-B unit (`has`) are ranked
-// (v_mbcnt over their ballot) and their lane numbers listed in the wave's LDS rank table, so
-// the round runs ceil(ready / 16) steps instead of 4: in step j, lane L moves granule (L & 3) of
-// the unit of the (16 j + L/4)-th ready chunk.  Granules touching the slot edges are written
+// (v_mbcnt over their ballot) and listed in the wave's LDS rank table as fpos | lane (fpos is
+// a multiple of 64), so the round runs ceil(ready / 16) steps instead of 4: in step j, lane L
+// moves granule (L & 3) of the unit of the (16 j + L/4)-th ready chunk.  Granules touching the slot edges are written
 // byte by byte (first unit of a misaligned slot, capacity end).
 static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, const u32* wring,
                                                  const EncOut* wout, u32* wrank) {
@@ -106,7 +111,7 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
   const u32 ready = (u32)__builtin_popcountll(M);  // (wave-uniform: s_bcnt1)
   if (has) {
     const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(M >> 32), __builtin_amdgcn_mbcnt_lo((u32)M, 0u));
-    wrank[r] = lane;
+    wrank[r] = enc_fpos(e) | lane;
   }
   const u32 g = lane & 3;
 #pragma unroll
@@ -114,9 +119,9 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
     if (16 * j >= ready) break;  // (wave-uniform)
     const u32 k = 16 * j + (lane >> 2);
     const bool act = k < ready;
-    const u32 c = act ? wrank[k] : 0u;
-    const u32 fp = (u32)__shfl((int)e.fpos, c);
     if (act) {
+      const u32 rec = wrank[k];
+      const u32 c = rec & 63u, fp = rec & ~63u;
       // fp is a multiple of ENC_UNIT = 64 B, so the granule's first slot is a multiple of 4 and
       // its 4 dwords never wrap the ring: one address, two ds_read2 (st64 for column-major)
       const u32 slot = ((fp >> 2) + 4 * g) & (ENC_RING - 1);
@@ -143,19 +148,17 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
       }
     }
   }
-  e.fpos += has ? (u32)ENC_UNIT : 0u;
+  e.fthr += has ? 8u * ENC_UNIT : 0u;
 }
 
-// flush rounds until no lane's ring is above the threshold (wave-uniform call sites only)
+// a flush round when some lane's ring is at the threshold (wave-uniform call sites only).  One
+// round is enough: a ring never holds more than 4 * ENC_RING - 1 = 127 settled bytes past fpos
+// (the static_asserts above), so after it moved a unit every lane holds at most 63 < FLUSH_AT.
 static __device__ __forceinline__ void enc_flush(Enc& e, u32 lane, const u32* wring,
                                                  const EncOut* wout, u32* wrank) {
-  // (the first test stays inline in every caller: written as a plain while loop, the compiler
-  // shared one test block among the call sites and copied the coder state at each jump to it)
-  if (__builtin_expect(__any((int)enc_ready(e, FLUSH_AT)), 0)) {
-    do {
-      enc_round(e, enc_ready(e, ENC_UNIT), lane, wring, wout, wrank);
-    } while (__any((int)enc_ready(e, FLUSH_AT)));
-  }
+  static_assert(4 * ENC_RING - 1 - ENC_UNIT < FLUSH_AT, "one flush round must suffice");
+  if (__builtin_expect(__any((int)enc_ready(e, FLUSH_AT)), 0))
+    enc_round(e, enc_ready(e, ENC_UNIT), lane, wring, wout, wrank);
 }
 
 // One settled byte, with a conditional push (rare paths only).
@@ -436,7 +439,7 @@ __global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, co
   e.range = ~0ull;
   e.acc = 0;
   e.B = 8 * a;  // pad bytes in front of the slot (never stored)
-  e.fpos = 0;
+  e.fthr = 8u * FLUSH_AT;  // fpos = 0
   e.err = 0;
   e.ring = (u32)(uintptr_t)(__attribute__((address_space(3))) u32*)(s_ring + wave * ENC_RING * 64 +
                                                                      ring_col(lane));
@@ -531,7 +534,8 @@ __global__ __launch_bounds__(WG, ENC_WAVES) void k_encode_static(ModelArgs m, co
   // final rounds: the last (partial) units, clipped to the stream end
   const u32 end = a + len;
   if (end < s_out[tid].hi_ok) s_out[tid].hi_ok = end;
-  while (__any((int)(e.fpos < wend))) enc_round(e, e.fpos < wend, lane, wring, wout, wrank);
+  while (__any((int)(enc_fpos(e) < wend)))
+    enc_round(e, enc_fpos(e) < wend, lane, wring, wout, wrank);
   RC_STAMP_END(enc, blockIdx.x * WAVES + wave, lane, n);
   if (live) {
     if (SM == 1) e.err = (e.err >> 24) ? enc_first_error(m, sp, n) : 0u;
