@@ -139,11 +139,16 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
         g16.w = v.w;
         gstore128(o.gbase + p0, g16);
       } else {
-        const u32 w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int b = 0; b < 16; ++b) {
+        // (rare: the first unit of a misaligned slot, the capacity end) a rolled loop, byte b
+        // of the granule in the low byte of r.x: this path is inlined at every flush site, and
+        // unrolled it made the encoder's symbol loops too large to unroll themselves
+        uint4 r = v;
+#pragma unroll 1
+        for (u32 b = 0; b < 16; ++b) {
           const u32 p = p0 + b;
-          if (p >= o.lo_ok && p < o.hi_ok) gstore8(o.gbase + p, w[b >> 2] >> (8 * (b & 3)));
+          if (p >= o.lo_ok && p < o.hi_ok) gstore8(o.gbase + p, r.x);
+          r = make_uint4(__builtin_amdgcn_alignbit(r.y, r.x, 8), __builtin_amdgcn_alignbit(r.z, r.y, 8),
+                         __builtin_amdgcn_alignbit(r.w, r.z, 8), r.w >> 8);
         }
       }
     }
@@ -328,8 +333,7 @@ static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const u
   // loop would select w[i >> 2] with v_cndmask_b32 on VCC (~13 extra SIMD cycles each)
   u32 w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
   uint2 t = s_tab[w0 & 255u];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  auto quarter = [&](int q) {
     if (ENC_PAIR && SM) {
       // table entries two symbols ahead (the pair's second and the next pair's first)
 #pragma unroll
@@ -353,6 +357,15 @@ static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const u
     w0 = w1;
     w1 = w2;
     w2 = w3;
+  };
+  // Small models: all four quarters unrolled (the word rotation then costs nothing); wide models
+  // hold more state, and unrolled four times their encoder spills, so they unroll by two
+  if (SM) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) quarter(q);
+  } else {
+#pragma unroll 2
+    for (int q = 0; q < 4; ++q) quarter(q);
   }
 }
 
