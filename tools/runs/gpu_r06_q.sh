@@ -1,4 +1,4 @@
-# Round 6, call Q: end-of-round evidence for the build with the ranked encoder flush and the segment-clamped decoder loads: the
+# Round 6, call Q: end-of-round evidence for the final build (ranked encoder flush, rolled slow path, segment-clamped decoder loads): the
 # bench under rocprofv3 (kernel stats) and the traffic counter passes for the headline (Zipf)
 # and the uniform load, the bound counters (Zipf, uniform, the N = 8 shard), the strong-scaling
 # sweep, and the N = 2 rank path rehearsed on one device at the real configs[4] size.

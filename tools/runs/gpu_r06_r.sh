@@ -15,3 +15,5 @@ python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py > $O/bench_rocprof.json 2> $O/bench_rocprof.err || { tail -20 $O/bench_rocprof.err; exit 1; }
 tail -1 $O/bench_rocprof.json | cut -c1-300
+timeout -k 10 480 python3 -u tools/parity_soak.py 360 20261020 > $O/parity_soak.log 2>&1 || { tail -5 $O/parity_soak.log; exit 1; }
+tail -1 $O/parity_soak.log | cut -c1-200
