@@ -103,8 +103,8 @@ struct EncOut {
 // One flush round.  The chunks of the wave that hold a complete 64-B unit (`has`) are ranked
 // (v_mbcnt over their ballot) and listed in the wave's LDS rank table as fpos | lane (fpos is
 // a multiple of 64), so the round runs ceil(ready / 16) steps instead of 4: in step j, lane L
-// moves granule (L & 3) of the unit of the (16 j + L/4)-th ready chunk.  Granules touching the slot edges are written
-// byte by byte (first unit of a misaligned slot, capacity end).
+// moves granule (L & 3) of the unit of the (16 j + L/4)-th ready chunk.  Granules touching the
+// slot edges are written byte by byte (first unit of a misaligned slot, capacity end).
 static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, const u32* wring,
                                                  const EncOut* wout, u32* wrank) {
   const u64 M = __builtin_amdgcn_ballot_w64(has);
@@ -147,7 +147,8 @@ static __device__ __forceinline__ void enc_round(Enc& e, bool has, u32 lane, con
         for (u32 b = 0; b < 16; ++b) {
           const u32 p = p0 + b;
           if (p >= o.lo_ok && p < o.hi_ok) gstore8(o.gbase + p, r.x);
-          r = make_uint4(__builtin_amdgcn_alignbit(r.y, r.x, 8), __builtin_amdgcn_alignbit(r.z, r.y, 8),
+          r = make_uint4(__builtin_amdgcn_alignbit(r.y, r.x, 8),
+                         __builtin_amdgcn_alignbit(r.z, r.y, 8),
                          __builtin_amdgcn_alignbit(r.w, r.z, 8), r.w >> 8);
         }
       }
