@@ -133,3 +133,40 @@ def test_encoder_on_ring_fixtures(ctx):
         want = bytes.fromhex(fx["chunks"][k % len(fx["chunks"])]["encoded_hex"])
         assert fl[k] == 0 and ol[k] == len(want), k
         assert bytes(out[out_off[k]:out_off[k] + ol[k]]) == want, k
+
+
+@pytest.mark.parametrize("name", ["zipf", "uniform"])
+def test_capacity_end_mid_stream_with_busy_flush_rounds(ctx, name):
+    """Slots that end deep inside their streams, on 320 ragged chunks (five waves, so each flush
+    round ranks many ready chunks, rc_encode.hip enc_round): RC_F_CAPACITY with the exact
+    length, and the slot holds the oracle stream's first cap bytes (encoder.rs:24-46).  The
+    slots are adjacent and misaligned, so a byte written past a slot's end would show in the
+    next slot's bytes."""
+    rng = np.random.default_rng(29)
+    if name == "zipf":
+        w = 1.0 / np.arange(1, 257) ** 1.2
+        c = np.maximum(1, np.floor(w / w.sum() * 65536)).astype(np.int64)
+        c[0] += 65536 - int(c.sum())
+        c = c.astype(np.uint32)
+    else:
+        c = np.ones(256, np.uint32)
+    total = int(c.astype(np.uint64).sum())
+    cum = cum_of(c)
+    m = rc.StaticModel(c, cum, total)
+    p = c / c.sum()
+    chunks = [rng.choice(256, size=int(rng.integers(2000, 9000)), p=p).astype(np.uint8)
+              for _ in range(320)]
+    want = [cpu.encode(c, cum, total, ch) for ch in chunks]
+    caps = []
+    for k, (f, b, L) in enumerate(want):
+        assert f == 0
+        caps.append(int(rng.integers(L // 4, L)) if k % 2 else L + int(rng.integers(0, 80)))
+    out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=True, seed=31)
+    for k, (f, b, L) in enumerate(want):
+        assert ol[k] == L, (name, k)
+        if caps[k] < L:
+            assert fl[k] == rc.api.N.F_CAPACITY, (name, k, fl[k])
+            assert bytes(out[out_off[k]:out_off[k] + caps[k]]) == b[:caps[k]], (name, k)
+        else:
+            assert fl[k] == 0, (name, k, fl[k])
+            assert bytes(out[out_off[k]:out_off[k] + L]) == b, (name, k)
