@@ -2,7 +2,7 @@
 # Round 6, call T: the driver's bench command on the final build, on another box (the spread)
 set -e
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06t
+O=gpurun_out/${RUN_TAG:-r06t}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 sha256sum range_coder_rust_amd/librc_amd.so > $O/lib.sha256
