@@ -224,7 +224,8 @@ static __device__ __forceinline__ void enc_out(Enc& e, u32 lh, u32 nb) {
 // lower bound before the shift) and nb (the bits that settle), shifts the state, and returns
 // true when the lane needs enc_rare() (after enc_out of this symbol).
 // SM: 0 wide model; 1 small model (256 <= total <= 2^16) that may hold entries the reference
-// cannot encode; 2 small and complete (256 symbols, every c > 0: nothing to check)
+// cannot encode; 2 small and complete (256 symbols, every c > 0: nothing to check); 3 the flat
+// model (complete, every c = 1, total 256: enc_tab synthesises the entries)
 template <int DIV, int SM>
 static __device__ __forceinline__ bool enc_core(Enc& e, const ModelArgs& m, uint2 t, u32& lh_out,
                                                 u32& nb_out) {
@@ -232,7 +233,7 @@ static __device__ __forceinline__ bool enc_core(Enc& e, const ModelArgs& m, uint
   RC_FILLER(e.fill);
 #endif
   u32 c, cum;
-  if (SM == 2) {
+  if (SM >= 2) {  // (3: the flat model, c = 1 folds the range product away)
     cum = t.x;
     c = t.y;
   } else if (SM) {  // bad entries were staged as (flag << 24, 1): accumulate, sort out at the end
@@ -273,6 +274,13 @@ static __device__ __forceinline__ bool enc_core(Enc& e, const ModelArgs& m, uint
   // settle; only range_reduction_expansion can be pending
   if (SM) return hi32(e.range) < 0x10000u;
   return (z > 31u) | (hi32(e.range) < 0x10000u);
+}
+
+// a symbol's (cum, c): the model's table entry; SM 3, the flat model (256 symbols, every c = 1,
+// total 256): (s, 1) with no table read
+template <int SM>
+static __device__ __forceinline__ uint2 enc_tab(const uint2* s_tab, u32 s) {
+  return SM == 3 ? make_uint2(s, 1u) : s_tab[s];
 }
 
 // one symbol, output included
@@ -333,15 +341,15 @@ static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const u
   // the words rotate down (w0 holds the current 4 symbols) instead of being indexed: a rolled
   // loop would select w[i >> 2] with v_cndmask_b32 on VCC (~13 extra SIMD cycles each)
   u32 w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-  uint2 t = s_tab[w0 & 255u];
+  uint2 t = enc_tab<SM>(s_tab, w0 & 255u);
   auto quarter = [&](int q) {
     if (ENC_PAIR && SM) {
       // table entries two symbols ahead (the pair's second and the next pair's first)
 #pragma unroll
       for (int i = 0; i < 4; i += 2) {
-        const uint2 t1 = s_tab[(w0 >> (8 * (i + 1))) & 255u];
+        const uint2 t1 = enc_tab<SM>(s_tab, (w0 >> (8 * (i + 1))) & 255u);
         const u32 sn = i < 2 ? (w0 >> (8 * (i + 2))) & 255u : w1 & 255u;
-        const uint2 tn = s_tab[sn];  // (past the tile's end: a harmless extra read)
+        const uint2 tn = enc_tab<SM>(s_tab, sn);  // (past the tile's end: a harmless extra read)
         enc_sym2<DIV, SM>(e, m, t, t1, act, lane, wring, wout, wrank);
         t = tn;
       }
@@ -349,7 +357,7 @@ static __device__ __forceinline__ void enc16(Enc& e, const ModelArgs& m, const u
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const u32 sn = i < 3 ? (w0 >> (8 * (i + 1))) & 255u : w1 & 255u;
-        const uint2 tn = s_tab[sn];  // (past the tile's end: a harmless extra read)
+        const uint2 tn = enc_tab<SM>(s_tab, sn);  // (past the tile's end: a harmless extra read)
         enc_sym<DIV, SM>(e, m, t, act, lane, wring, wout, wrank);
         t = tn;
       }
@@ -377,7 +385,7 @@ static __device__ __forceinline__ void enc_byte_sym(Enc& e, const ModelArgs& m,
                                                     bool act, u32 lane, const u32* wring,
                                                     const EncOut* wout, u32* wrank) {
   const u32 sym = act ? (u32)sp[i] : 0u;
-  enc_sym<DIV, SM>(e, m, s_tab[sym], act, lane, wring, wout, wrank);
+  enc_sym<DIV, SM>(e, m, enc_tab<SM>(s_tab, sym), act, lane, wring, wout, wrank);
 }
 
 // the first symbol of a chunk the reference cannot encode (rare: flagged chunks only)
@@ -591,10 +599,12 @@ hipError_t rc_static_encode_launch(hipStream_t stream, const RcKnobs& k, const M
   };
 #ifdef RC_DEV_ONLY  // scratch builds for kernel tuning: the headline variants only
   if (div != DIV_POW2 || smv == 0) return hipErrorInvalidValue;
-  if (smv == 2) go(k_encode_static<DIV_POW2, 2>); else go(k_encode_static<DIV_POW2, 1>);
+  if (a.flat) go(k_encode_static<DIV_POW2, 3>);
+  else if (smv == 2) go(k_encode_static<DIV_POW2, 2>); else go(k_encode_static<DIV_POW2, 1>);
 #else
   if (div == DIV_POW2) {
-    if (smv == 2) go(k_encode_static<DIV_POW2, 2>);
+    if (a.flat) go(k_encode_static<DIV_POW2, 3>);  // the flat model (SM 3: no table reads)
+    else if (smv == 2) go(k_encode_static<DIV_POW2, 2>);
     else if (smv == 1) go(k_encode_static<DIV_POW2, 1>);
     else go(k_encode_static<DIV_POW2, 0>);
   } else {

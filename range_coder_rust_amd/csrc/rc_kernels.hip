@@ -380,6 +380,10 @@ rc_status rc_model_create_static(rc_ctx* ctx, uint32_t n_symbols, const uint32_t
       }
       lut.swap(wide);
     }
+    // the flat model (raw bytes: configs[1]): cum[s] = s and c = 1 for every symbol
+    bool flat = n_symbols == 256 && total_freq == 256;
+    for (u32 i = 0; flat && i < 256; ++i) flat = c_freq[i] == 1;
+    a.flat = flat ? 1u : 0u;
   }
   // pair buckets (k_decode_static LUT 3, rc_static.h): 2^15 < total <= 2^16, so buckets of 16
   // frequencies, and every c < 2^16 (16-bit fields).  Per bucket both candidates of its bucket

@@ -102,6 +102,8 @@ struct ModelArgs {
   u32 prio_step;     //   s_setprio min(3, 1 + (b - prio_base) / prio_step); ~0: all at 0
   u32 prio_rot;      // set per launch: 0, or rotate priorities every 2^prio_rot ticks of the
                      // 100 MHz clock (rc_prio_rotate)
+  u32 flat;          // 1: the flat model (256 symbols, every c = 1, total 256): cum[s] = s, so
+                     // the coders need no table (k_decode_static LUT 5, k_encode_static FLAT)
 };
 
 // Wave priority ("the end of a launch").  Every chunk is one lane's serial stream

@@ -537,3 +537,36 @@ def test_pair_bucket_decoder_vs_oracle(ctx, knob_ctx, pair):
     same streams: decoded symbols against the oracle's, ragged and misaligned chunks; garbage
     streams decode like the reference's find_index, flags included."""
     _pair_decoder_cases(knob_ctx(RC_DEC_PAIR=pair))
+
+def test_flat_model_garbage_and_truncated_streams(ctx):
+    """The flat model (256 symbols, every c = 1: k_decode_static LUT 5, k_encode_static SM 3,
+    no table reads) on arbitrary bytes and truncated streams: flags as the oracle's, and the
+    decoded symbols where the oracle decodes (find_index is rfreq itself, sample_impl.rs:27-45)."""
+    rng = np.random.default_rng(41)
+    c = np.ones(256, np.uint32)
+    cum = cum_of(c)
+    m = rc.StaticModel(c, cum, 256)
+    codes = [rng.integers(0, 256, int(rng.integers(8, 600))).astype(np.uint8).tobytes()
+             for _ in range(96)]
+    counts = [int(rng.integers(0, 700)) for _ in codes]
+    dec, fd = run_decode(m, codes, counts, misalign=True, seed=41)
+    for k in range(len(codes)):
+        f, d = cpu.decode(c, cum, 256, codes[k], counts[k])
+        assert fd[k] == f, (k, fd[k], f)
+        if f == 0:
+            assert (dec[k] == d).all(), k
+    # valid streams cut short, and their encoder bytes against the oracle
+    chunks = [rng.integers(0, 256, int(rng.integers(1, 3000))).astype(np.uint8) for _ in range(64)]
+    caps = [rc.slot_capacity(len(ch), 9) for ch in chunks]
+    out, out_off, ol, fl = run_encode(m, chunks, caps, misalign=True, seed=43)
+    cut = []
+    for k, ch in enumerate(chunks):
+        f, b, L = cpu.encode(c, cum, 256, ch)
+        assert fl[k] == f == 0 and ol[k] == L and bytes(out[out_off[k]:out_off[k] + L]) == b, k
+        cut.append(b[:max(8, L - int(rng.integers(0, 6)))])
+    dec, fd = run_decode(m, cut, [len(ch) for ch in chunks], misalign=True, seed=47)
+    for k, ch in enumerate(chunks):
+        f, d = cpu.decode(c, cum, 256, cut[k], len(ch))
+        assert fd[k] == f, (k, fd[k], f)
+        if f == 0:
+            assert (dec[k] == ch).all(), k
