@@ -254,7 +254,8 @@ static __device__ __forceinline__ bool enc_core(Enc& e, const ModelArgs& m, uint
     const u32 rl = (u32)r, rh = hi32(r);
     const u64 R0 = (u64)rl * c;                   // range_coder.rs:65
     const u64 L0 = (u64)rl * cum + e.low;         // range_coder.rs:68-81 (no overflow, §3)
-    e.range = ((u64)(hi32(R0) + __umul24(rh, c)) << 32) | (u32)R0;
+    // (the flat model: range = r * 1, written out: __umul24's operand mask would stay)
+    e.range = SM == 3 ? r : ((u64)(hi32(R0) + __umul24(rh, c)) << 32) | (u32)R0;
     e.low = ((u64)(hi32(L0) + __umul24(rh, cum)) << 32) | (u32)L0;
   } else {
     e.range = r * (u64)c;
